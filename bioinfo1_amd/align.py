@@ -1,0 +1,298 @@
+"""Python host-side mirror of the team_alignment interface.
+
+``align()`` mirrors ``team::Align`` (/root/reference/team_alignment/
+team_alignment.hpp:14-23): same arguments, same results -- the int score, the
+CIGAR bytes the reference assigns to ``*cigar`` (``None`` when no CIGAR is
+requested, like passing ``cigar = nullptr``) and ``*target_begin`` -- and the
+same error: an unknown type raises ``ValueError("Unknown AlignmentType
+provided.")`` (the reference's ``std::invalid_argument``).
+
+``Aligner.align_batch()`` is the batched form (host memory in and out) and
+``DevicePlan`` the device-resident form (torch CUDA tensors in HBM) used by
+bench.py.  Everything goes through the extern "C" ABI of
+``libteam_alignment.so`` (include/team_align_c.h) into the gfx950 HIP
+kernels; there is no CPU fallback -- if the library or a gfx950 GPU is
+missing, these raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import enum
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libteam_alignment.so")
+
+TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY = range(6)
+
+
+class AlignmentType(enum.IntEnum):
+    """team::AlignmentType (team_alignment.hpp:8-12), underlying int."""
+
+    global_ = 0
+    local = 1
+    semiGlobal = 2
+
+
+class DeviceError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load libteam_alignment.so (fails loudly if it was not built).
+
+    torch, when importable, is imported first so that the process has a single
+    HIP runtime (torch's libamdhip64 satisfies the library's dependency)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    L = C.CDLL(LIB_PATH)
+    u32p, u64p, i32p = C.POINTER(C.c_uint32), C.POINTER(C.c_uint64), C.POINTER(C.c_int32)
+    L.ta_status_string.restype = C.c_char_p
+    L.ta_status_string.argtypes = [C.c_int]
+    L.ta_last_error.restype = C.c_char_p
+    L.ta_last_error.argtypes = [C.c_void_p]
+    L.ta_context_create.argtypes = [C.c_int, C.POINTER(C.c_void_p)]
+    L.ta_context_destroy.argtypes = [C.c_void_p]
+    L.ta_context_destroy.restype = None
+    L.ta_cigar_slot_bytes.restype = C.c_uint64
+    L.ta_cigar_slot_bytes.argtypes = [C.c_uint32, C.c_uint32]
+    L.ta_align_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, u64p, u32p, C.c_void_p, u64p, u32p, C.c_int,
+                                 C.c_int, C.c_int, C.c_int, C.c_int, i32p, u32p, C.c_void_p, C.c_uint64, u64p, u32p]
+    L.ta_plan_create.argtypes = [C.c_void_p, C.c_uint32, u32p, u32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
+                                 C.c_uint64, C.POINTER(C.c_void_p)]
+    L.ta_plan_destroy.argtypes = [C.c_void_p]
+    L.ta_plan_destroy.restype = None
+    for f in ("ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes"):
+        getattr(L, f).restype = C.c_uint64
+        getattr(L, f).argtypes = [C.c_void_p]
+    L.ta_plan_chunks.restype = C.c_uint32
+    L.ta_plan_chunks.argtypes = [C.c_void_p]
+    L.ta_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ta_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+    L.ta_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+    _lib = L
+    return L
+
+
+# Every symbol include/team_align_c.h declares (checked by tests/test_abi.py).
+ABI_SYMBOLS = [
+    "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_cigar_slot_bytes",
+    "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes",
+    "ta_plan_chunks", "ta_plan_execute", "ta_plan_execute_fill", "ta_plan_execute_traceback",
+]
+# The drop-in C++ entry point (team_alignment.hpp), g++/libstdc++ cxx11 mangling.
+TEAM_ALIGN_SYMBOL = ("_ZN4team5AlignEPKcjS1_jNS_13AlignmentTypeEiiiPNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEEPj")
+
+
+def _check_type(type) -> int:
+    t = int(type)
+    if t not in (0, 1, 2):
+        raise ValueError("Unknown AlignmentType provided.")
+    return t
+
+
+def _raise(status: int, ctx=None):
+    L = lib()
+    msg = L.ta_status_string(status).decode()
+    if status in (TA_ERR_BAD_TYPE, TA_ERR_CIGAR):
+        raise ValueError(msg)
+    detail = L.ta_last_error(ctx).decode() if ctx else ""
+    raise DeviceError(f"{msg}: {detail}" if detail else msg)
+
+
+def _p(a, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+@dataclass
+class BatchResult:
+    scores: np.ndarray  # int32 [P]
+    target_begins: np.ndarray  # uint32 [P]
+    cigar_offsets: np.ndarray | None  # uint64 [P]
+    cigar_lens: np.ndarray | None  # uint32 [P]
+    arena: np.ndarray | None  # uint8
+
+    def cigar(self, p: int) -> bytes | None:
+        if self.arena is None:
+            return None
+        o = int(self.cigar_offsets[p])
+        return self.arena[o : o + int(self.cigar_lens[p])].tobytes()
+
+    def cigars(self):
+        return [self.cigar(p) for p in range(len(self.scores))]
+
+
+class Aligner:
+    """A device context (HIP stream + staging buffers) on one gfx950 GPU."""
+
+    def __init__(self, device: int = 0):
+        L = lib()
+        h = C.c_void_p()
+        r = L.ta_context_create(device, C.byref(h))
+        if r != TA_OK:
+            raise DeviceError(f"ta_context_create(device={device}): {L.ta_status_string(r).decode()}")
+        self._h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ta_context_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def align_batch(self, batch, type, match: int, mismatch: int, gap: int, want_cigar: bool = True) -> BatchResult:
+        """Batched team::Align over a bioinfo1_amd.synth.PairBatch."""
+        L = lib()
+        t = _check_type(type)
+        P = batch.n_pairs
+        sc = np.zeros(P, np.int32)
+        tb = np.zeros(P, np.uint32)
+        coff = clen = arena = None
+        cap = 0
+        if want_cigar:
+            cap = int((2 * (batch.qlen.astype(np.uint64) + batch.tlen.astype(np.uint64)) + 2).sum()) if P else 0
+            arena = np.zeros(max(cap, 1), np.uint8)
+            coff = np.zeros(P, np.uint64)
+            clen = np.zeros(P, np.uint32)
+        qb = batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8)
+        tbb = batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8)
+        r = L.ta_align_batch(
+            self._h, P, qb.ctypes.data, _p(batch.qoff, C.c_uint64), _p(batch.qlen, C.c_uint32), tbb.ctypes.data,
+            _p(batch.toff, C.c_uint64), _p(batch.tlen, C.c_uint32), t, match, mismatch, gap, int(bool(want_cigar)),
+            _p(sc, C.c_int32), _p(tb, C.c_uint32), arena.ctypes.data if want_cigar else None, cap,
+            _p(coff, C.c_uint64) if want_cigar else None, _p(clen, C.c_uint32) if want_cigar else None)
+        if r != TA_OK:
+            _raise(r, self._h)
+        return BatchResult(sc, tb, coff, clen, arena)
+
+
+_default: Aligner | None = None
+
+
+def default_aligner() -> Aligner:
+    global _default
+    if _default is None:
+        _default = Aligner(0)
+    return _default
+
+
+def align(query: bytes, target: bytes, type, match: int, mismatch: int, gap: int, want_cigar: bool = True):
+    """team::Align for one pair -> (score, cigar bytes or None, target_begin)."""
+    from .synth import from_pairs
+
+    _check_type(type)
+    res = default_aligner().align_batch(from_pairs([(bytes(query), bytes(target))]), type, match, mismatch, gap,
+                                        want_cigar)
+    return int(res.scores[0]), res.cigar(0), int(res.target_begins[0])
+
+
+class _DeviceIO(C.Structure):
+    _fields_ = [("query_bytes", C.c_void_p), ("query_off", C.c_void_p), ("target_bytes", C.c_void_p),
+                ("target_off", C.c_void_p), ("score", C.c_void_p), ("target_begin", C.c_void_p),
+                ("cigar_slots", C.c_void_p), ("cigar_start", C.c_void_p), ("cigar_len", C.c_void_p)]
+
+
+class DevicePlan:
+    """Device-resident batch: inputs and outputs are torch tensors in HBM.
+
+    Mirrors the mapper-side batching of SURVEY §8f: lengths and scoring are
+    fixed at plan time; ``run()`` enqueues the fill + traceback kernels on the
+    current torch stream (asynchronous)."""
+
+    def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, device=None,
+                 workspace_budget: int = 0):
+        import torch
+
+        L = lib()
+        t = _check_type(type)
+        self.torch = torch
+        self.dev = torch.device("cuda", aligner.device) if device is None else device
+        self.P = batch.n_pairs
+        self.want_cigar = bool(want_cigar)
+        h = C.c_void_p()
+        r = L.ta_plan_create(aligner.handle, self.P, _p(batch.qlen, C.c_uint32), _p(batch.tlen, C.c_uint32), t,
+                             match, mismatch, gap, int(self.want_cigar), workspace_budget, C.byref(h))
+        if r != TA_OK:
+            _raise(r, aligner.handle)
+        self._h = h
+        self._ctx = aligner.handle
+        f = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)  # noqa: E731
+        self.qbytes = f(batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8))
+        self.tbytes = f(batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8))
+        self.qoff = f(batch.qoff.view(np.int64))
+        self.toff = f(batch.toff.view(np.int64))
+        self.score = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
+        self.target_begin = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
+        self.slots_bytes = int(L.ta_plan_cigar_slots_bytes(h))
+        self.slots = torch.zeros(max(self.slots_bytes, 1) if self.want_cigar else 1, dtype=torch.uint8,
+                                 device=self.dev)
+        self.cigar_start = torch.zeros(self.P, dtype=torch.int64, device=self.dev)
+        self.cigar_len = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
+        self.io = _DeviceIO(self.qbytes.data_ptr(), self.qoff.data_ptr(), self.tbytes.data_ptr(),
+                            self.toff.data_ptr(), self.score.data_ptr(), self.target_begin.data_ptr(),
+                            self.slots.data_ptr(), self.cigar_start.data_ptr(), self.cigar_len.data_ptr())
+        self.workspace_bytes = int(L.ta_plan_workspace_bytes(h))
+        self.chunks = int(L.ta_plan_chunks(h))
+
+    def _stream(self):
+        return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
+
+    def run(self):
+        r = lib().ta_plan_execute(self._h, C.byref(self.io), self._stream())
+        if r != TA_OK:
+            _raise(r, self._ctx)
+
+    def run_fill(self, chunk: int = 0):
+        r = lib().ta_plan_execute_fill(self._h, C.byref(self.io), self._stream(), chunk)
+        if r != TA_OK:
+            _raise(r, self._ctx)
+
+    def run_traceback(self, chunk: int = 0):
+        r = lib().ta_plan_execute_traceback(self._h, C.byref(self.io), self._stream(), chunk)
+        if r != TA_OK:
+            _raise(r, self._ctx)
+
+    def results(self) -> BatchResult:
+        """Synchronise and copy results to host (CIGARs unpacked from slots)."""
+        self.torch.cuda.synchronize(self.dev)
+        sc = self.score.cpu().numpy()
+        tb = self.target_begin.cpu().numpy().view(np.uint32)
+        if not self.want_cigar:
+            return BatchResult(sc, tb, None, None, None)
+        start = self.cigar_start.cpu().numpy().view(np.uint64)
+        ln = self.cigar_len.cpu().numpy().view(np.uint32)
+        slots = self.slots.cpu().numpy()
+        return BatchResult(sc, tb, start, ln, slots)
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ta_plan_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,424 @@
+// bioinfo1_amd/csrc/ta_api.hip -- host side of the extern "C" ABI
+// (include/team_align_c.h): contexts, batch plans, workspace layout, chunking
+// and the host-memory batch entry point.  The DP itself is in ta_kernels.hip.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/team_align_c.h"
+#include "ta_internal.h"
+
+struct ta_context {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::string last_error;
+    std::mutex mu;  // one batch at a time per context
+    // grow-only device staging for ta_align_batch
+    struct Buf {
+        void* p = nullptr;
+        size_t cap = 0;
+    };
+    Buf qbytes, tbytes, qoff, toff, score, tb, slots, cstart, clen, dst_off, dst;
+};
+
+struct ta_plan {
+    ta_context* ctx = nullptr;
+    uint32_t n_pairs = 0;
+    int type = 0, match = 0, mismatch = 0, gap = 0;
+    bool want_cigar = false, wide = false;
+    std::vector<uint32_t> qlen, tlen, order;
+    std::vector<uint64_t> slot_off;
+    struct Chunk {
+        uint32_t begin, count;
+        uint64_t ptr_dwords, bnd_words;
+    };
+    std::vector<Chunk> chunks;
+    uint64_t slots_bytes = 0, ws_ptr_dwords = 0, ws_bnd_words = 0;
+    // device
+    uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr;
+    uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
+    uint32_t *d_goal_i = nullptr, *d_goal_j = nullptr;
+    uint32_t* d_ptrs = nullptr;
+    int32_t* d_bnd = nullptr;
+};
+
+namespace {
+
+int fail(ta_context* ctx, int code, const std::string& msg) {
+    if (ctx) ctx->last_error = msg;
+    return code;
+}
+
+#define TA_HIP(ctx, expr)                                                                            \
+    do {                                                                                             \
+        hipError_t e_ = (expr);                                                                      \
+        if (e_ != hipSuccess)                                                                        \
+            return fail((ctx), TA_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+bool valid_type(int t) { return t == TA_GLOBAL || t == TA_LOCAL || t == TA_SEMI_GLOBAL; }
+
+uint64_t default_budget() {
+    if (const char* e = std::getenv("TA_WORKSPACE_BYTES")) return std::strtoull(e, nullptr, 10);
+    return 48ull << 30;  // of the 288 GB HBM
+}
+
+int grow(ta_context* ctx, ta_context::Buf& b, size_t bytes) {
+    if (bytes <= b.cap) return TA_OK;
+    if (b.p) (void)hipFree(b.p);
+    b.p = nullptr;
+    b.cap = 0;
+    size_t want = std::max<size_t>(bytes, 4096);
+    TA_HIP(ctx, hipMalloc(&b.p, want));
+    b.cap = want;
+    return TA_OK;
+}
+
+template <class T>
+int upload(ta_context* ctx, T** dptr, const std::vector<T>& v) {
+    if (v.empty()) return TA_OK;
+    TA_HIP(ctx, hipMalloc(reinterpret_cast<void**>(dptr), v.size() * sizeof(T)));
+    TA_HIP(ctx, hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return TA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ta_status_string(int status) {
+    switch (status) {
+        case TA_OK: return "ok";
+        case TA_ERR_BAD_TYPE: return "Unknown AlignmentType provided.";
+        case TA_ERR_CIGAR: return "Unknown error in determining cigar string.";
+        case TA_ERR_ARG: return "invalid argument";
+        case TA_ERR_DEVICE: return "device error";
+        case TA_ERR_CAPACITY: return "cigar arena too small";
+        default: return "unknown status";
+    }
+}
+
+const char* ta_last_error(const ta_context* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+uint64_t ta_cigar_slot_bytes(uint32_t n, uint32_t m) { return ta::cigar_slot_bytes(n, m); }
+
+int ta_context_create(int device, ta_context** out) {
+    if (!out) return TA_ERR_ARG;
+    *out = nullptr;
+    int count = 0;
+    if (hipGetDeviceCount(&count) != hipSuccess || count <= device || device < 0) return TA_ERR_DEVICE;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return TA_ERR_DEVICE;
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TA_ERR_DEVICE;  // kernels are gfx950-only
+    auto* c = new ta_context();
+    c->device = device;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return TA_ERR_DEVICE;
+    }
+    *out = c;
+    return TA_OK;
+}
+
+void ta_context_destroy(ta_context* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    for (auto* b : {&ctx->qbytes, &ctx->tbytes, &ctx->qoff, &ctx->toff, &ctx->score, &ctx->tb, &ctx->slots,
+                    &ctx->cstart, &ctx->clen, &ctx->dst_off, &ctx->dst})
+        if (b->p) (void)hipFree(b->p);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+void ta_plan_destroy(ta_plan* pl) {
+    if (!pl) return;
+    (void)hipSetDevice(pl->ctx->device);
+    for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_ptr_off,
+                    (void*)pl->d_bnd_off, (void*)pl->d_slot_off, (void*)pl->d_goal_i, (void*)pl->d_goal_j,
+                    (void*)pl->d_ptrs, (void*)pl->d_bnd})
+        if (p) (void)hipFree(p);
+    delete pl;
+}
+
+int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
+                   int match, int mismatch, int gap, int want_cigar, uint64_t budget, ta_plan** out) {
+    if (!ctx || !out || (n_pairs && (!qlen || !tlen))) return fail(ctx, TA_ERR_ARG, "null argument");
+    *out = nullptr;
+    if (!valid_type(type)) return fail(ctx, TA_ERR_BAD_TYPE, ta_status_string(TA_ERR_BAD_TYPE));
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    auto* pl = new ta_plan();
+    pl->ctx = ctx;
+    pl->n_pairs = n_pairs;
+    pl->type = type;
+    pl->match = match;
+    pl->mismatch = mismatch;
+    pl->gap = gap;
+    pl->want_cigar = want_cigar != 0;
+    pl->qlen.assign(qlen, qlen + n_pairs);
+    pl->tlen.assign(tlen, tlen + n_pairs);
+    // Local mode packs (score << 5 | row) into 32 bits; take the unpacked
+    // argmax when any local score could reach 2^26.
+    uint64_t maxlen = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) maxlen = std::max<uint64_t>(maxlen, (uint64_t)qlen[p] + tlen[p]);
+    const uint64_t mag = std::max<uint64_t>({1ull, (uint64_t)std::llabs(match), (uint64_t)std::llabs(mismatch),
+                                             (uint64_t)std::llabs(gap)});
+    pl->wide = (type == TA_LOCAL) && (maxlen * mag >= (1ull << 26));
+    // Longest pairs first (fewer stragglers), stable for equal cell counts.
+    pl->order.resize(n_pairs);
+    std::iota(pl->order.begin(), pl->order.end(), 0u);
+    std::stable_sort(pl->order.begin(), pl->order.end(), [&](uint32_t a, uint32_t b) {
+        return (uint64_t)pl->qlen[a] * pl->tlen[a] > (uint64_t)pl->qlen[b] * pl->tlen[b];
+    });
+    if (budget == 0) budget = default_budget();
+    const uint64_t budget_dw = std::max<uint64_t>(budget / 4, 1);
+    std::vector<uint64_t> ptr_off(n_pairs, 0), bnd_off(n_pairs, 0);
+    pl->slot_off.assign(n_pairs, 0);
+    uint64_t so = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        pl->slot_off[p] = so;
+        so += ta::cigar_slot_bytes(pl->qlen[p], pl->tlen[p]);
+    }
+    pl->slots_bytes = so;
+    ta_plan::Chunk cur{0, 0, 0, 0};
+    for (uint32_t k = 0; k < n_pairs; ++k) {
+        const uint32_t p = pl->order[k];
+        const uint64_t pd = pl->want_cigar ? ta::ptr_dwords(pl->qlen[p], pl->tlen[p]) : 0;
+        const uint64_t bw = ta::bnd_words(pl->qlen[p], pl->tlen[p]);
+        if (cur.count && cur.ptr_dwords + pd > budget_dw) {
+            pl->chunks.push_back(cur);
+            cur = ta_plan::Chunk{k, 0, 0, 0};
+        }
+        ptr_off[p] = cur.ptr_dwords;
+        bnd_off[p] = cur.bnd_words;
+        cur.ptr_dwords += pd;
+        cur.bnd_words += bw;
+        ++cur.count;
+    }
+    if (cur.count) pl->chunks.push_back(cur);
+    for (auto& c : pl->chunks) {
+        pl->ws_ptr_dwords = std::max(pl->ws_ptr_dwords, c.ptr_dwords);
+        pl->ws_bnd_words = std::max(pl->ws_bnd_words, c.bnd_words);
+    }
+    int rc = TA_OK;
+    auto up = [&](int r) {
+        if (r != TA_OK && rc == TA_OK) rc = r;
+    };
+    up(upload(ctx, &pl->d_qlen, pl->qlen));
+    up(upload(ctx, &pl->d_tlen, pl->tlen));
+    up(upload(ctx, &pl->d_order, pl->order));
+    up(upload(ctx, &pl->d_ptr_off, ptr_off));
+    up(upload(ctx, &pl->d_bnd_off, bnd_off));
+    up(upload(ctx, &pl->d_slot_off, pl->slot_off));
+    if (rc == TA_OK && n_pairs) {
+        if (hipMalloc(&pl->d_goal_i, n_pairs * 4ull) != hipSuccess ||
+            hipMalloc(&pl->d_goal_j, n_pairs * 4ull) != hipSuccess)
+            rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc goal");
+    }
+    if (rc == TA_OK && pl->ws_ptr_dwords &&
+        hipMalloc(&pl->d_ptrs, pl->ws_ptr_dwords * 4ull) != hipSuccess)
+        rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc pointer workspace");
+    if (rc == TA_OK && pl->ws_bnd_words && hipMalloc(&pl->d_bnd, pl->ws_bnd_words * 4ull) != hipSuccess)
+        rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc boundary workspace");
+    if (rc != TA_OK) {
+        ta_plan_destroy(pl);
+        return rc;
+    }
+    *out = pl;
+    return TA_OK;
+}
+
+uint64_t ta_plan_cigar_slots_bytes(const ta_plan* pl) { return pl ? pl->slots_bytes : 0; }
+uint64_t ta_plan_workspace_bytes(const ta_plan* pl) {
+    return pl ? (pl->ws_ptr_dwords + pl->ws_bnd_words) * 4ull : 0;
+}
+uint32_t ta_plan_chunks(const ta_plan* pl) { return pl ? (uint32_t)pl->chunks.size() : 0; }
+
+static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill, bool trace) {
+    const auto& ch = pl->chunks[c];
+    if (fill) {
+        ta::FillArgs a{};
+        a.order = pl->d_order;
+        a.begin = ch.begin;
+        a.count = ch.count;
+        a.qbytes = reinterpret_cast<const uint8_t*>(io->query_bytes);
+        a.qoff = io->query_off;
+        a.qlen = pl->d_qlen;
+        a.tbytes = reinterpret_cast<const uint8_t*>(io->target_bytes);
+        a.toff = io->target_off;
+        a.tlen = pl->d_tlen;
+        a.match = pl->match;
+        a.mismatch = pl->mismatch;
+        a.gap = pl->gap;
+        a.ptrs = pl->d_ptrs;
+        a.ptr_off = pl->d_ptr_off;
+        a.bnd = pl->d_bnd;
+        a.bnd_off = pl->d_bnd_off;
+        a.score = io->score;
+        a.target_begin = io->target_begin;
+        a.goal_i = pl->d_goal_i;
+        a.goal_j = pl->d_goal_j;
+        TA_HIP(pl->ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, a, s));
+    }
+    if (trace && pl->want_cigar) {
+        ta::TraceArgs t{};
+        t.order = pl->d_order;
+        t.begin = ch.begin;
+        t.count = ch.count;
+        t.qlen = pl->d_qlen;
+        t.tlen = pl->d_tlen;
+        t.ptrs = pl->d_ptrs;
+        t.ptr_off = pl->d_ptr_off;
+        t.goal_i = pl->d_goal_i;
+        t.goal_j = pl->d_goal_j;
+        t.slots = io->cigar_slots;
+        t.slot_off = pl->d_slot_off;
+        t.cigar_start = io->cigar_start;
+        t.cigar_len = io->cigar_len;
+        TA_HIP(pl->ctx, ta::launch_traceback(pl->type, t, s));
+    }
+    return TA_OK;
+}
+
+static int check_io(ta_plan* pl, const ta_device_io* io) {
+    if (!pl || !io) return TA_ERR_ARG;
+    if (pl->n_pairs && (!io->query_off || !io->target_off || !io->score || !io->target_begin))
+        return fail(pl->ctx, TA_ERR_ARG, "null device pointer");
+    if (pl->want_cigar && pl->n_pairs && (!io->cigar_slots || !io->cigar_start || !io->cigar_len))
+        return fail(pl->ctx, TA_ERR_ARG, "null cigar device pointer");
+    return TA_OK;
+}
+
+int ta_plan_execute(ta_plan* pl, const ta_device_io* io, void* stream) {
+    if (int r = check_io(pl, io)) return r;
+    TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
+    hipStream_t s = stream ? (hipStream_t)stream : pl->ctx->stream;
+    for (uint32_t c = 0; c < pl->chunks.size(); ++c)
+        if (int r = exec_chunk(pl, io, s, c, true, true)) return r;
+    return TA_OK;
+}
+
+int ta_plan_execute_fill(ta_plan* pl, const ta_device_io* io, void* stream, uint32_t chunk) {
+    if (int r = check_io(pl, io)) return r;
+    if (chunk >= pl->chunks.size()) return pl->n_pairs ? TA_ERR_ARG : TA_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : pl->ctx->stream;
+    return exec_chunk(pl, io, s, chunk, true, false);
+}
+
+int ta_plan_execute_traceback(ta_plan* pl, const ta_device_io* io, void* stream, uint32_t chunk) {
+    if (int r = check_io(pl, io)) return r;
+    if (chunk >= pl->chunks.size()) return pl->n_pairs ? TA_ERR_ARG : TA_OK;
+    hipStream_t s = stream ? (hipStream_t)stream : pl->ctx->stream;
+    return exec_chunk(pl, io, s, chunk, false, true);
+}
+
+int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff, const uint32_t* qlen,
+                   const char* tbytes, const uint64_t* toff, const uint32_t* tlen, int type, int match,
+                   int mismatch, int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* arena,
+                   uint64_t arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len) {
+    if (!ctx) return TA_ERR_ARG;
+    if (!valid_type(type)) return fail(ctx, TA_ERR_BAD_TYPE, ta_status_string(TA_ERR_BAD_TYPE));
+    if (n_pairs == 0) return TA_OK;
+    if (!qoff || !qlen || !toff || !tlen) return fail(ctx, TA_ERR_ARG, "null input array");
+    if (want_cigar && (!arena || !cigar_off || !cigar_len)) return fail(ctx, TA_ERR_ARG, "null cigar output");
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    // input extents
+    uint64_t qend = 0, tend = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        qend = std::max<uint64_t>(qend, qoff[p] + qlen[p]);
+        tend = std::max<uint64_t>(tend, toff[p] + tlen[p]);
+    }
+    if ((qend && !qb) || (tend && !tbytes)) return fail(ctx, TA_ERR_ARG, "null sequence bytes");
+    ta_plan* pl = nullptr;
+    if (int r = ta_plan_create(ctx, n_pairs, qlen, tlen, type, match, mismatch, gap, want_cigar, 0, &pl)) return r;
+    int rc = TA_OK;
+    auto chk = [&](int r) {
+        if (r != TA_OK && rc == TA_OK) rc = r;
+        return rc == TA_OK;
+    };
+    const size_t P = n_pairs;
+    if (chk(grow(ctx, ctx->qbytes, qend)) && chk(grow(ctx, ctx->tbytes, tend)) &&
+        chk(grow(ctx, ctx->qoff, P * 8)) && chk(grow(ctx, ctx->toff, P * 8)) && chk(grow(ctx, ctx->score, P * 4)) &&
+        chk(grow(ctx, ctx->tb, P * 4)) &&
+        (!want_cigar || (chk(grow(ctx, ctx->slots, pl->slots_bytes)) && chk(grow(ctx, ctx->cstart, P * 8)) &&
+                         chk(grow(ctx, ctx->clen, P * 4)) && chk(grow(ctx, ctx->dst_off, P * 8))))) {
+        auto cp = [&](void* d, const void* h, size_t b) {
+            if (!b || rc != TA_OK) return;
+            hipError_t e = hipMemcpyAsync(d, h, b, hipMemcpyHostToDevice, s);
+            if (e != hipSuccess) rc = fail(ctx, TA_ERR_DEVICE, hipGetErrorString(e));
+        };
+        cp(ctx->qbytes.p, qb, qend);
+        cp(ctx->tbytes.p, tbytes, tend);
+        cp(ctx->qoff.p, qoff, P * 8);
+        cp(ctx->toff.p, toff, P * 8);
+        ta_device_io io{};
+        io.query_bytes = (const char*)ctx->qbytes.p;
+        io.query_off = (const uint64_t*)ctx->qoff.p;
+        io.target_bytes = (const char*)ctx->tbytes.p;
+        io.target_off = (const uint64_t*)ctx->toff.p;
+        io.score = (int32_t*)ctx->score.p;
+        io.target_begin = (uint32_t*)ctx->tb.p;
+        io.cigar_slots = (char*)ctx->slots.p;
+        io.cigar_start = (uint64_t*)ctx->cstart.p;
+        io.cigar_len = (uint32_t*)ctx->clen.p;
+        if (rc == TA_OK) chk(ta_plan_execute(pl, &io, s));
+        std::vector<int32_t> sc(P);
+        std::vector<uint32_t> tb(P);
+        auto dn = [&](void* h, const void* d, size_t b) {
+            if (!b || rc != TA_OK) return;
+            hipError_t e = hipMemcpyAsync(h, d, b, hipMemcpyDeviceToHost, s);
+            if (e != hipSuccess) rc = fail(ctx, TA_ERR_DEVICE, hipGetErrorString(e));
+        };
+        dn(sc.data(), io.score, P * 4);
+        dn(tb.data(), io.target_begin, P * 4);
+        if (want_cigar) dn(cigar_len, io.cigar_len, P * 4);
+        if (rc == TA_OK) {
+            hipError_t e = hipStreamSynchronize(s);
+            if (e != hipSuccess) rc = fail(ctx, TA_ERR_DEVICE, hipGetErrorString(e));
+        }
+        if (rc == TA_OK && want_cigar) {
+            uint64_t total = 0;
+            for (size_t p = 0; p < P; ++p) {
+                cigar_off[p] = total;
+                total += cigar_len[p];
+            }
+            if (total > arena_bytes) {
+                rc = fail(ctx, TA_ERR_CAPACITY, "cigar arena too small");
+            } else if (chk(grow(ctx, ctx->dst, total))) {
+                cp(ctx->dst_off.p, cigar_off, P * 8);
+                ta::CompactArgs ca{};
+                ca.n_pairs = n_pairs;
+                ca.slots = io.cigar_slots;
+                ca.cigar_start = io.cigar_start;
+                ca.cigar_len = io.cigar_len;
+                ca.dst_off = (const uint64_t*)ctx->dst_off.p;
+                ca.dst = (char*)ctx->dst.p;
+                if (rc == TA_OK) {
+                    hipError_t e = ta::launch_compact(ca, s);
+                    if (e != hipSuccess) rc = fail(ctx, TA_ERR_DEVICE, hipGetErrorString(e));
+                }
+                dn(arena, ctx->dst.p, total);
+                if (rc == TA_OK) {
+                    hipError_t e = hipStreamSynchronize(s);
+                    if (e != hipSuccess) rc = fail(ctx, TA_ERR_DEVICE, hipGetErrorString(e));
+                }
+            }
+        }
+        if (rc == TA_OK) {
+            if (score) std::memcpy(score, sc.data(), P * 4);
+            if (target_begin) std::memcpy(target_begin, tb.data(), P * 4);
+        }
+    }
+    ta_plan_destroy(pl);
+    return rc;
+}
+
+}  // extern "C"

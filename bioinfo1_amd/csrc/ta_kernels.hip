@@ -1,0 +1,552 @@
+// bioinfo1_amd/csrc/ta_kernels.hip -- gfx950 kernels for the team::Align path.
+//
+// What they compute is team::Align (/root/reference/team_alignment/
+// team_alignment.cpp:49-350) for a batch of independent pairs:
+//   fill      -- the (n+1)x(m+1) int32 DP of :102-116 / :171-194 / :249-264
+//                (strict-> tie order MATCH > INSERT > DELETE, local clamp at 0,
+//                '-' makes a gap free), the goal cell of :117-121 / :186-199 /
+//                :265-285, the score and target_begin; with CIGAR on it also
+//                writes a 2-bit traceback code per cell to HBM.
+//   traceback -- the parent walk of :123-138 / :201-217 / :286-315 (incl. the
+//                semi-global trailing I/D), run-length encoded (:145-160) into
+//                the pair's CIGAR slot.
+//   compact   -- packs the per-pair CIGAR slots back to back (host batches).
+//
+// How: one wave64 per pair.  Lane l owns 16 consecutive query
+// rows ("stripe"); lanes sweep the target columns with a one-step lane skew
+// (lane l is at column t-l+1 at step t), so each lane's row-0 "up" and
+// "diag" neighbours are lane l-1's last row one and two steps earlier.  They
+// move with one DPP wave_shr:1 per step -- no LDS, no shuffles through memory.
+// Target characters enter at lane 0 and ride the same shift.  The pointer
+// bits of a cell come from VALU compares whose wave-wide lane masks are
+// combined on the SALU (canonical code M/I/D/STOP) and accumulated per lane,
+// 16 rows x 2 bits = one dword per lane per step, stored as one coalesced
+// 256-byte row per step.  Queries longer than 1024 rows take several passes;
+// the bottom row of a pass is handed to the next through a boundary row in HBM.
+#include <climits>
+#include <type_traits>
+
+#include "ta_internal.h"
+
+namespace ta {
+namespace {
+
+__device__ __forceinline__ int wadd(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int wmul(uint32_t a, int b) { return (int)(a * (uint32_t)b); }
+
+// DPP wave_shr:1 -- lane l gets v of lane l-1, lane 0 gets `lane0`.
+// Must run with all 64 lanes enabled.
+__device__ __forceinline__ int wave_shr1(int lane0, int v) {
+    return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ int rdlane(int v, uint32_t l) { return __builtin_amdgcn_readlane(v, (int)l); }
+
+// Global wave index.  readfirstlane tells the compiler it is wave-uniform
+// (threadIdx.x >> 6 is not provably so), which keeps the pair's lengths, the
+// loop counters and all per-pair control flow in SGPRs / scalar branches.
+__device__ __forceinline__ uint32_t wave_id() {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
+// acc*2 + (this lane's bit of `mask`) in one v_addc_co_u32 (the lane mask is
+// the carry-in).  hipcc does not form this from C++ (it emits a cndmask +
+// shift + or), so it is spelled out.
+__device__ __forceinline__ uint32_t shl1_add_lanebit(uint32_t acc, uint64_t mask) {
+    uint32_t r;
+    uint64_t carry_out;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(carry_out) : "v"(acc), "s"(mask));
+    return r;
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int first_lane(bool c) {
+    const unsigned long long b = __ballot(c);
+    return b ? __ffsll((long long)b) - 1 : -1;
+}
+
+// 256 target characters per chunk, 4 per lane; out-of-range bytes are 0.
+__device__ __forceinline__ uint32_t load_tchunk(const uint8_t* T, uint32_t m, uint32_t k, int lane) {
+    const uint32_t base = k * 256u + 4u * (uint32_t)lane;
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t idx = base + b;
+        const uint32_t c = idx < m ? (uint32_t)T[idx] : 0u;
+        w |= c << (8 * b);
+    }
+    return w;
+}
+
+// 64 boundary-row values per chunk: column 64k+lane+1.
+__device__ __forceinline__ int load_bchunk(const int32_t* B, uint32_t m, uint32_t k, int lane) {
+    const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+    return j <= m ? B[j] : 0;
+}
+
+// Degenerate pairs (an empty query or target): closed forms of what the
+// reference computes when one of its loops is empty.
+template <int MODE>
+__device__ void degenerate(const FillArgs& a, uint32_t p, uint32_t n, uint32_t m) {
+    int score = 0;
+    uint32_t gi = 0, gj = 0, tb = 0;
+    if (MODE == kGlobal) {  // :117-121 goal (n,m); boundary cost (n or m)*gap
+        gi = n;
+        gj = m;
+        score = n ? wmul(n, a.gap) : wmul(m, a.gap);
+    } else if (MODE == kLocal) {  // max never set: goal (0,0), tb = 0+1
+        tb = 1;
+    } else {  // :265-278: (0,m) wins the column scan (cost 0); row scan never beats it
+        gi = 0;
+        gj = (n == 0) ? m : 0;
+    }
+    a.score[p] = score;
+    a.target_begin[p] = tb;
+    a.goal_i[p] = gi;
+    a.goal_j[p] = gj;
+}
+
+// Select v[idx] for a wave-uniform runtime idx without dynamic register
+// indexing (which the compiler would lower through LDS or scratch).
+template <int R>
+__device__ __forceinline__ int select_row(const int (&v)[R], uint32_t idx) {
+    int x = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) x |= v[k] & -(int)(idx == (uint32_t)k);
+    return x;
+}
+
+// What one pass reports to the running goal.
+struct PassOut {
+    int h;           // local: best score of the pass; semi: best of column m
+    uint32_t i, j;   // its cell (1-based rows), i == 0 when no candidate
+    int row_h;       // semi, last pass: best of row n
+    uint32_t row_j;
+    int corner;      // global, last pass: H[n][m]
+};
+
+// One pass = rows row_base+1 .. row_base+nrows of the query against the whole
+// target.  NV = valid rows of the last lane in use (compile-time, so every
+// register index below is static).
+template <int MODE, bool CIGAR, bool WIDE, int NV>
+__device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
+                                            uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
+                                            int32_t* B, int lane) {
+    constexpr int R = kRows;
+    const int ma = a.match, mi = a.mismatch, gap = a.gap;
+    const int init = (MODE == kGlobal) ? gap : 0;  // :58-74
+    const uint32_t Tmax = pass_steps(m);
+    const uint32_t row_base = pass * kPassRows;
+    const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
+    const uint32_t nl = (nrows + R - 1) / R;  // lanes in use; lane nl-1 holds NV valid rows
+    const bool has_next = !last_pass;
+
+    int qc[R], gq[R], H[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i0 = row_base + (uint32_t)lane * R + r;  // query index of row i0+1
+        qc[r] = i0 < n ? (int)Q[i0] : 0x100;                    // 0x100 never equals a byte
+        gq[r] = (qc[r] == '-') ? 0 : gap;                       // indel(q[i-1]) :25-28
+        H[r] = wmul(i0 + 1, init);                               // column 0, :83-86
+    }
+    int recv = wmul(row_base + (uint32_t)lane * R, init);  // H[row above the stripe][0]
+    int tc = 0x100;
+    const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
+
+    uint32_t bestkey = 0, bestj = 0;  // local: key = h<<5 | (16-r)
+    int bh = INT_MIN;                 // local, WIDE: unpacked (h, r, j)
+    uint32_t br = 0, bj = 0;
+    int rowbest = INT_MIN;            // semi: row n
+    uint32_t rowbest_j = 0;
+
+    uint32_t tcur = load_tchunk(T, m, 0, lane), tnext = load_tchunk(T, m, 1, lane);
+    int bcur = 0, bnext = 0;
+    if (pass > 0) {
+        bcur = load_bchunk(B, m, 0, lane);
+        bnext = load_bchunk(B, m, 1, lane);
+    }
+    const uint32_t steps = m + nl - 1;
+    const uint64_t step_base = (uint64_t)pass * Tmax;
+
+    // One step = one target column per lane (lane l at column t-l+1).
+    // MASKED steps (the ramp-up / ramp-down of the lane skew) run the cell
+    // update under the per-lane `active` exec mask; in the steady state every
+    // lane in use is active and lanes >= nl compute throw-away values, so
+    // the update runs unmasked and H is updated in place.
+    auto step = [&](uint32_t t, auto masked_tag) {
+        constexpr bool MASKED = decltype(masked_tag)::value;
+        if ((t & 255u) == 0 && t) {
+            tcur = tnext;
+            tnext = load_tchunk(T, m, (t >> 8) + 1, lane);
+        }
+        int top;
+        if (pass == 0) {
+            top = wmul(t + 1, init);  // row 0, :89-92
+        } else {
+            if ((t & 63u) == 0 && t) {
+                bcur = bnext;
+                bnext = load_bchunk(B, m, (t >> 6) + 1, lane);
+            }
+            top = rdlane(bcur, t & 63u);
+        }
+        const uint32_t word = (uint32_t)rdlane((int)tcur, (t >> 2) & 63u);
+        const int newc = (int)((word >> ((t & 3u) * 8)) & 0xFFu);
+        const int prev = recv;
+        recv = wave_shr1(top, H[R - 1]);
+        tc = wave_shr1(newc, tc);
+
+        const int j = (int)t - lane + 1;
+        const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
+        uint32_t acc = 0;
+        if (active) {
+            const int gt = (tc == '-') ? 0 : gap;  // indel(t[j-1])
+            int dg = prev, upv = recv;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int old = H[r];
+                const int s = (qc[r] == tc) ? ma : mi;  // match_func :20-23
+                const int diag = wadd(dg, s);
+                const int left = wadd(old, gt);
+                const int up = wadd(upv, gq[r]);
+                const int m1 = max(diag, left);
+                int h = max(m1, up);
+                if (MODE == kLocal) h = max(h, 0);  // :185
+                if (CIGAR) {
+                    // wave-wide lane masks from the VALU compares; the
+                    // canonical code is formed on the SALU:
+                    //   hi = D | S,  lo = (I & !D) | S   (M=00 I=01 D=10 STOP=11)
+                    const uint64_t mD = ballot(up > m1);      // DELETE only if strictly greater
+                    const uint64_t mI = ballot(left > diag);  // INSERT beats MATCH only if strictly greater
+                    uint64_t hi = mD, lo = mI & ~mD;
+                    if (MODE == kLocal) {
+                        const uint64_t mS = ballot(h == 0);   // cost 0 ends the local walk
+                        hi |= mS;
+                        lo |= mS;
+                    }
+                    acc = shl1_add_lanebit(acc, hi);
+                    acc = shl1_add_lanebit(acc, lo);
+                }
+                if (MODE == kLocal && WIDE) {
+                    if ((uint32_t)r < nv_lane && (h > bh || (h == bh && (uint32_t)r < br))) {
+                        bh = h;
+                        br = r;
+                        bj = (uint32_t)j;
+                    }
+                }
+                H[r] = h;
+                dg = old;
+                upv = h;
+            }
+            if (MODE == kLocal && !WIDE) {
+                // key = h*32 + (16-r): larger score first, then the smaller row;
+                // strict '>' over steps keeps the first column (:186).
+                uint32_t P[R];
+                P[0] = ((uint32_t)H[0] << 5) | (uint32_t)R;
+#pragma unroll
+                for (int r = 1; r < R; ++r) P[r] = max(P[r - 1], ((uint32_t)H[r] << 5) | (uint32_t)(R - r));
+                uint32_t sk = P[R - 1];
+                if (NV != R) sk = ((uint32_t)lane == nl - 1) ? P[NV - 1] : sk;
+                if (sk > bestkey) {
+                    bestkey = sk;
+                    bestj = (uint32_t)j;
+                }
+            }
+            if (MODE == kSemi && (NV != R || last_pass)) {
+                // row n is register NV-1 of lane nl-1 in the last pass
+                if (H[NV - 1] > rowbest) {
+                    rowbest = H[NV - 1];
+                    rowbest_j = (uint32_t)j;
+                }
+            }
+            if (has_next && (uint32_t)lane == nl - 1) B[j] = H[R - 1];
+        }
+        if (CIGAR) ptrs[(step_base + t) * kWave + lane] = acc;
+    };
+    // lanes 0..nl-1 are all active for t in [nl-1, m-1]
+    const uint32_t ramp_end = min(nl - 1, steps);
+    uint32_t t = 0;
+    for (; t < ramp_end; ++t) step(t, std::true_type{});
+    for (; t < m; ++t) step(t, std::false_type{});
+    for (; t < steps; ++t) step(t, std::true_type{});
+
+    PassOut o{INT_MIN, 0, 0, INT_MIN, 0, 0};
+    if (MODE == kLocal) {
+        const int v = (uint32_t)lane >= nl ? INT_MIN : (WIDE ? bh : (bestkey ? (int)(bestkey >> 5) : -1));
+        const int mx = wave_max(v);
+        const int fl = first_lane(v == mx);
+        uint32_t r, j;
+        if (!WIDE) {
+            r = R - ((uint32_t)rdlane((int)bestkey, fl) & 31u);
+            j = (uint32_t)rdlane((int)bestj, fl);
+        } else {
+            r = (uint32_t)rdlane((int)br, fl);
+            j = (uint32_t)rdlane((int)bj, fl);
+        }
+        o.h = mx;
+        o.i = row_base + (uint32_t)fl * R + r + 1;
+        o.j = j;
+    } else if (MODE == kSemi) {
+        // column m (H holds it now), i ascending, strict '>' (:265-270)
+        int cv = INT_MIN;
+        uint32_t cr = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if ((uint32_t)r < nv_lane && H[r] > cv) {
+                cv = H[r];
+                cr = r;
+            }
+        const int mx = wave_max(cv);
+        const int fl = first_lane(cv == mx && nv_lane > 0);
+        o.h = mx;
+        o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane((int)cr, fl) + 1;
+        o.j = m;
+        if (last_pass) {
+            o.row_h = rdlane(rowbest, nl - 1);
+            o.row_j = (uint32_t)rdlane((int)rowbest_j, nl - 1);
+        }
+    } else {
+        if (last_pass) o.corner = rdlane(select_row<R>(H, NV - 1), nl - 1);
+    }
+    return o;
+}
+
+template <int MODE, bool CIGAR, bool WIDE>
+__device__ __forceinline__ PassOut run_pass_nv(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
+                                            uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
+                                            int32_t* B, int lane) {
+    const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
+    const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
+    // Global needs NV only for the corner cell, which run_pass reads with a
+    // runtime select; local/semi specialise the step loop on NV.
+    if (MODE == kGlobal || nv == kRows) return run_pass<MODE, CIGAR, WIDE, kRows>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
+#define TA_NV_CASE(k) \
+    case k: return run_pass<MODE, CIGAR, WIDE, k>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
+    switch (nv) {
+        TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
+        TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
+        default: TA_NV_CASE(15)
+    }
+#undef TA_NV_CASE
+}
+
+template <int MODE, bool CIGAR, bool WIDE>
+__global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t widx = wave_id();
+    if (widx >= a.count) return;  // wave-uniform
+    const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
+    const uint32_t n = a.qlen[p], m = a.tlen[p];
+    if (n == 0 || m == 0) {
+        if (lane == 0) degenerate<MODE>(a, p, n, m);
+        return;
+    }
+    const uint8_t* Q = a.qbytes + a.qoff[p];
+    const uint8_t* T = a.tbytes + a.toff[p];
+    const uint32_t passes = n_passes(n);
+    uint32_t* ptrs = CIGAR ? a.ptrs + a.ptr_off[p] : nullptr;
+    int32_t* B = (passes > 1) ? a.bnd + a.bnd_off[p] : nullptr;
+
+    // running goal over passes (wave-uniform); semi starts from (0,m), cost 0
+    int best_h = (MODE == kSemi) ? 0 : INT_MIN;
+    uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
+    int corner = 0;
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        const bool last_pass = pass + 1 == passes;
+        const PassOut o = run_pass_nv<MODE, CIGAR, WIDE>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
+        if (MODE != kGlobal && o.h > best_h) {  // strict: the earlier (upper) pass wins ties
+            best_h = o.h;
+            best_i = o.i;
+            best_j = o.j;
+        }
+        if (MODE == kSemi && last_pass && o.row_h > best_h) {  // row n after column m (:271-278)
+            best_h = o.row_h;
+            best_i = n;
+            best_j = o.row_j;
+        }
+        if (MODE == kGlobal && last_pass) corner = o.corner;
+        // the next pass reads this pass's bottom row (written by this wave)
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    }
+    if (lane == 0) {
+        a.score[p] = (MODE == kGlobal) ? corner : best_h;
+        a.target_begin[p] = (MODE == kLocal) ? best_j + 1 : 0;  // :117-121 / :197-199 / :283-285
+        a.goal_i[p] = (MODE == kGlobal) ? n : best_i;
+        a.goal_j[p] = (MODE == kGlobal) ? m : best_j;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Traceback: one wave per pair, the walk itself is wave-uniform (SALU); the
+// wave's lanes only fetch 64-step x 4-lane tiles of the pointer matrix
+// (64 rows x ~64 columns) with one dwordx4 load each, and the walk reads codes
+// out of the tile with v_readlane.  The CIGAR is written right to left.
+struct RleWriter {
+    char* slot;
+    uint64_t pos;
+    uint32_t op, cnt;
+    uint64_t total;
+    int lane;
+    __device__ void put(char c) {
+        --pos;
+        if (lane == 0) slot[pos] = c;
+    }
+    __device__ void flush() {
+        if (!cnt) return;
+        put((char)op);  // to_string(count) + op, written backwards
+        uint32_t c = cnt;
+        do {
+            put((char)('0' + c % 10u));
+            c /= 10u;
+        } while (c);
+    }
+    __device__ void push(uint32_t o, uint32_t k) {
+        if (!k) return;
+        total += k;
+        if (o == op) {
+            cnt += k;
+        } else {
+            flush();
+            op = o;
+            cnt = k;
+        }
+    }
+};
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t widx = wave_id();
+    if (widx >= a.count) return;
+    const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
+    const uint32_t n = a.qlen[p], m = a.tlen[p];
+    const uint32_t gi = a.goal_i[p], gj = a.goal_j[p];
+    const uint64_t cap = cigar_slot_bytes(n, m);
+    RleWriter w{a.slots + a.slot_off[p], cap, 0u, 0u, 0ull, lane};
+    if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
+        if (gi == n) w.push('I', m - gj);
+        else if (gj == m) w.push('D', n - gi);
+    }
+    const uint32_t* P = a.ptrs + a.ptr_off[p];
+    const uint32_t Tmax = pass_steps(m);
+    uint32_t i = gi, j = gj;
+    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tq = 0;
+    uint4 tile = make_uint4(0, 0, 0, 0);
+    while (true) {
+        if (MODE == kLocal) {
+            if (i == 0 || j == 0) break;  // row/col 0 cost 0 ends the walk (:202)
+        } else {
+            if (i == 0) {  // row 0: INSERT parents (:89-92)
+                w.push('I', j);
+                break;
+            }
+            if (j == 0) {  // column 0: DELETE parents (:83-86)
+                w.push('D', i);
+                break;
+            }
+        }
+        const uint32_t row = i - 1;
+        const uint32_t pass = row / kPassRows;
+        const uint32_t within = row % kPassRows;
+        const uint32_t ln = within / kRows, r = within % kRows;
+        const uint32_t t = (j - 1) + ln;
+        if (!(pass == tP && t >= tt0 && t < tt0 + 64u && (ln >> 2) == tq)) {
+            tP = pass;
+            tq = ln >> 2;
+            tt0 = t >= 63u ? t - 63u : 0u;
+            const uint32_t ts = tt0 + (uint32_t)lane;
+            tile = make_uint4(0, 0, 0, 0);
+            if (ts < Tmax)
+                tile = *reinterpret_cast<const uint4*>(P + ((uint64_t)pass * Tmax + ts) * kWave + tq * 4u);
+        }
+        const uint32_t sel = ln & 3u;
+        const uint32_t comp = sel == 0 ? tile.x : sel == 1 ? tile.y : sel == 2 ? tile.z : tile.w;
+        const uint32_t dw = (uint32_t)rdlane((int)comp, t - tt0);
+        const uint32_t code = (dw >> (2u * (kRows - 1 - r))) & 3u;
+        if (code == kCodeStop) break;  // local: cost == 0 (:202)
+        if (code == kCodeM) {
+            w.push('M', 1);
+            --i;
+            --j;
+        } else if (code == kCodeI) {
+            w.push('I', 1);
+            --j;
+        } else {
+            w.push('D', 1);
+            --i;
+        }
+    }
+    w.flush();
+    if (w.total == 0) {  // RLE of an empty string: "1" + '\0' (:145-160)
+        w.put('\0');
+        w.put('1');
+    }
+    if (lane == 0) {
+        a.cigar_start[p] = a.slot_off[p] + w.pos;
+        a.cigar_len[p] = (uint32_t)(cap - w.pos);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t p = wave_id();
+    if (p >= a.n_pairs) return;
+    const char* src = a.slots + a.cigar_start[p];
+    char* dst = a.dst + a.dst_off[p];
+    const uint32_t len = a.cigar_len[p];
+    for (uint32_t k = (uint32_t)lane; k < len; k += 64u) dst[k] = src[k];
+}
+
+inline dim3 grid_for(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock); }
+
+template <int MODE>
+hipError_t launch_fill_mode(bool cigar, bool wide, const FillArgs& a, hipStream_t s) {
+    if (!a.count) return hipSuccess;
+    const dim3 g = grid_for(a.count), b(kBlock);
+    if (cigar) {
+        if (wide) hipLaunchKernelGGL((fill_kernel<MODE, true, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((fill_kernel<MODE, true, false>), g, b, 0, s, a);
+    } else {
+        if (wide) hipLaunchKernelGGL((fill_kernel<MODE, false, true>), g, b, 0, s, a);
+        else hipLaunchKernelGGL((fill_kernel<MODE, false, false>), g, b, 0, s, a);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s) {
+    // WIDE only changes the local argmax; other modes use one instantiation.
+    switch (mode) {
+        case kGlobal: return launch_fill_mode<kGlobal>(cigar, false, a, s);
+        case kLocal: return launch_fill_mode<kLocal>(cigar, wide, a, s);
+        case kSemi: return launch_fill_mode<kSemi>(cigar, false, a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s) {
+    if (!a.count) return hipSuccess;
+    const dim3 g = grid_for(a.count), b(kBlock);
+    switch (mode) {
+        case kGlobal: hipLaunchKernelGGL(traceback_kernel<kGlobal>, g, b, 0, s, a); break;
+        case kLocal: hipLaunchKernelGGL(traceback_kernel<kLocal>, g, b, 0, s, a); break;
+        case kSemi: hipLaunchKernelGGL(traceback_kernel<kSemi>, g, b, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
+    if (!a.n_pairs) return hipSuccess;
+    hipLaunchKernelGGL(compact_kernel, grid_for(a.n_pairs), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+
+}  // namespace ta

@@ -1,0 +1,124 @@
+/*
+ * include/team_align_c.h -- extern "C" batch ABI of the MI355X team_alignment
+ * engine (libteam_alignment.so).
+ *
+ * This is the boundary the reference's Align() path is replaced behind.  The
+ * reference exposes one C++ entry, team::Align
+ * (/root/reference/team_alignment/team_alignment.hpp:14-23, implemented at
+ * team_alignment.cpp:49-350), called once per read by team_mapper.cpp:666,
+ * 674, 755, 763.  Each function below states which part of that interface it
+ * replaces.  Plain pointers and sizes only; no C++ or torch types; nothing
+ * throws.  Every function returns a TA_* status.
+ *
+ * Semantics per pair are exactly team::Align's:
+ *   score        -- the int the reference returns
+ *   target_begin -- what the reference writes to *target_begin
+ *                   (0 for global/semiGlobal, end column + 1 for local)
+ *   CIGAR        -- the bytes the reference assigns to *cigar: decimal run
+ *                   lengths of M / I (consumes target) / D (consumes query);
+ *                   an empty alignment is the 2-byte string "1\0".
+ */
+#ifndef TEAM_ALIGN_C_H
+#define TEAM_ALIGN_C_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* team::AlignmentType values (team_alignment.hpp:8-12). */
+#define TA_GLOBAL 0
+#define TA_LOCAL 1
+#define TA_SEMI_GLOBAL 2
+
+/* Status codes. */
+#define TA_OK 0
+#define TA_ERR_BAD_TYPE 1 /* reference: std::invalid_argument("Unknown AlignmentType provided.") */
+#define TA_ERR_CIGAR 2    /* reference: std::invalid_argument("Unknown error in determining cigar string.") */
+#define TA_ERR_ARG 3      /* null pointer / inconsistent sizes */
+#define TA_ERR_DEVICE 4   /* no usable gfx950 device or a HIP runtime failure (see ta_last_error) */
+#define TA_ERR_CAPACITY 5 /* caller-provided CIGAR arena too small */
+
+typedef struct ta_context ta_context; /* device + stream + cached buffers; one per host thread */
+typedef struct ta_plan ta_plan;       /* a batch's lengths, scoring and device workspace layout */
+
+/* Message for a status code (static storage). */
+const char* ta_status_string(int status);
+/* Last error detail recorded on this context (e.g. the HIP error string). */
+const char* ta_last_error(const ta_context* ctx);
+
+/* Create a context on HIP device `device` (gfx950 required).  Replaces nothing
+ * in the reference (which has no device state); team::Align keeps one per
+ * calling thread so concurrent callers (team_mapper.cpp:596 OpenMP) are safe. */
+int ta_context_create(int device, ta_context** out);
+void ta_context_destroy(ta_context* ctx);
+
+/* Bytes of the per-pair CIGAR slot for an n x m pair: 2*(n+m)+2, an upper
+ * bound on any run-length CIGAR of that pair (team_alignment.cpp:145-160). */
+uint64_t ta_cigar_slot_bytes(uint32_t query_len, uint32_t target_len);
+
+/*
+ * Host-memory batch: the batched form of team::Align
+ * (team_alignment.hpp:14-23), n_pairs independent calls with shared
+ * type/match/mismatch/gap.  Inputs are SoA: concatenated bytes + per-pair
+ * offset + length (length-delimited, not NUL-terminated, as Align takes them).
+ * Outputs (host memory, n_pairs each): score[], target_begin[] (either may be
+ * NULL, like Align's optional pointer), and when want_cigar != 0 the CIGARs
+ * packed back to back into cigar_arena (capacity cigar_arena_bytes; at most
+ * the sum of ta_cigar_slot_bytes is ever needed), pair p's bytes at
+ * cigar_arena[cigar_off[p] .. cigar_off[p]+cigar_len[p]).
+ * want_cigar == 0 is the reference's cigar == nullptr mode: no traceback.
+ * Returns TA_ERR_BAD_TYPE for an unknown type (no pair is computed).
+ */
+int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, const uint64_t* query_off,
+                   const uint32_t* query_len, const char* target_bytes, const uint64_t* target_off,
+                   const uint32_t* target_len, int type, int match, int mismatch, int gap, int want_cigar,
+                   int32_t* score, uint32_t* target_begin, char* cigar_arena, uint64_t cigar_arena_bytes,
+                   uint64_t* cigar_off, uint32_t* cigar_len);
+
+/*
+ * Device-resident batches (the mapper-side batching of SURVEY §8f and the
+ * benchmark path).  A plan fixes the lengths (host arrays, copied) and the
+ * scoring, lays out the device workspace (2-bit traceback pointers, pass
+ * boundary rows) and chunks the batch when the pointer matrices exceed
+ * workspace_budget bytes (0 = library default).
+ */
+int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
+                   const uint32_t* target_len_host, int type, int match, int mismatch, int gap, int want_cigar,
+                   uint64_t workspace_budget, ta_plan** out);
+void ta_plan_destroy(ta_plan* plan);
+/* Total bytes of the device CIGAR slot arena the caller must provide. */
+uint64_t ta_plan_cigar_slots_bytes(const ta_plan* plan);
+/* Device workspace held by the plan, and the number of launch chunks. */
+uint64_t ta_plan_workspace_bytes(const ta_plan* plan);
+uint32_t ta_plan_chunks(const ta_plan* plan);
+
+/* Device pointers for one execution of a plan. */
+typedef struct ta_device_io {
+    const char* query_bytes;      /* device */
+    const uint64_t* query_off;    /* device, n_pairs */
+    const char* target_bytes;     /* device */
+    const uint64_t* target_off;   /* device, n_pairs */
+    int32_t* score;               /* device, n_pairs */
+    uint32_t* target_begin;       /* device, n_pairs */
+    char* cigar_slots;            /* device, ta_plan_cigar_slots_bytes(); unused when !want_cigar */
+    uint64_t* cigar_start;        /* device, n_pairs: pair p's CIGAR starts at cigar_slots[cigar_start[p]] */
+    uint32_t* cigar_len;          /* device, n_pairs */
+} ta_device_io;
+
+/* Enqueue the whole batch on `hip_stream` (a hipStream_t; NULL = the
+ * context's stream).  Asynchronous: returns after enqueueing. */
+int ta_plan_execute(ta_plan* plan, const ta_device_io* io, void* hip_stream);
+
+/* Enqueue only the DP fill (scores/target_begin; traceback pointers into the
+ * workspace) or only the traceback, for profiling the two kernels. */
+int ta_plan_execute_fill(ta_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
+int ta_plan_execute_traceback(ta_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* TEAM_ALIGN_C_H */

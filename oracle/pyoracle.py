@@ -1,0 +1,149 @@
+"""ctypes bindings for the CPU checkers (TEST INFRASTRUCTURE ONLY).
+
+* ``Oracle``    -- oracle/liboracle.so, our C restatement (align_oracle.c)
+* ``Reference`` -- oracle/_ref/libref_align.so, the unmodified reference
+                   team_alignment.cpp compiled by oracle/Makefile (present
+                   only where it was built; it is never committed).
+Both expose ``align(q, t, type, match, mismatch, gap, want_cigar)`` ->
+(score, cigar_bytes_or_None, target_begin) and a batch call over a
+``bioinfo1_amd.synth.PairBatch``.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "liboracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libref_align.so")
+
+ERR_MSG = {1: "Unknown AlignmentType provided.", 2: "Unknown error in determining cigar string."}
+
+
+class AlignError(ValueError):
+    pass
+
+
+def build(force: bool = False) -> None:
+    if force or not os.path.exists(ORACLE_SO):
+        subprocess.check_call(["make", "-s", "-C", HERE], stdout=subprocess.DEVNULL)
+
+
+def cigar_bound(n: int, m: int) -> int:
+    return 2 * (n + m) + 2
+
+
+def _ptr(a, ct):
+    return a.ctypes.data_as(C.POINTER(ct))
+
+
+class _Base:
+    def _slots(self, batch):
+        cap = 2 * (batch.qlen.astype(np.uint64) + batch.tlen.astype(np.uint64)) + np.uint64(2)
+        off = np.zeros(batch.n_pairs, dtype=np.uint64)
+        if batch.n_pairs:
+            off[1:] = np.cumsum(cap[:-1], dtype=np.uint64)
+        total = int(cap.sum()) if batch.n_pairs else 0
+        return off, cap, np.zeros(max(total, 1), dtype=np.uint8)
+
+
+class Oracle(_Base):
+    kind = "port"
+
+    def __init__(self):
+        build()
+        lib = C.CDLL(ORACLE_SO)
+        lib.oracle_align.restype = C.c_int
+        lib.oracle_align.argtypes = [C.c_char_p, C.c_uint, C.c_char_p, C.c_uint, C.c_int, C.c_int, C.c_int,
+                                     C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint), C.c_char_p,
+                                     C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.oracle_align_batch.restype = C.c_int
+        lib.oracle_max_threads.restype = C.c_int
+        self.lib = lib
+
+    def max_threads(self) -> int:
+        return int(self.lib.oracle_max_threads())
+
+    def align(self, q: bytes, t: bytes, type: int, match: int, mismatch: int, gap: int, want_cigar=True):
+        cap = cigar_bound(len(q), len(t))
+        buf = C.create_string_buffer(cap)
+        sc, tb, cl = C.c_int(0), C.c_uint(0), C.c_size_t(0)
+        r = self.lib.oracle_align(q, len(q), t, len(t), int(type), match, mismatch, gap, int(bool(want_cigar)),
+                                  C.byref(sc), C.byref(tb), buf, cap, C.byref(cl))
+        if r:
+            raise AlignError(ERR_MSG.get(r, f"oracle status {r}"))
+        return sc.value, (buf.raw[: cl.value] if want_cigar else None), tb.value
+
+    def align_batch(self, batch, type, match, mismatch, gap, want_cigar=True, n_threads=0):
+        P = batch.n_pairs
+        off, cap, arena = self._slots(batch)
+        sc = np.zeros(P, np.int32)
+        tb = np.zeros(P, np.uint32)
+        cl = np.zeros(P, np.uint32)
+        st = np.zeros(P, np.int32)
+        self.lib.oracle_align_batch(
+            C.c_uint(P), _ptr(batch.qbytes, C.c_char), _ptr(batch.qoff, C.c_uint64), _ptr(batch.qlen, C.c_uint32),
+            _ptr(batch.tbytes, C.c_char), _ptr(batch.toff, C.c_uint64), _ptr(batch.tlen, C.c_uint32),
+            C.c_int(int(type)), C.c_int(match), C.c_int(mismatch), C.c_int(gap), C.c_int(int(bool(want_cigar))),
+            C.c_int(n_threads), _ptr(sc, C.c_int32), _ptr(tb, C.c_uint32), _ptr(arena, C.c_char),
+            _ptr(off, C.c_uint64), _ptr(cl, C.c_uint32), _ptr(st, C.c_int32))
+        return BatchResult(sc, tb, cl, st, arena, off, want_cigar)
+
+
+class Reference(_Base):
+    kind = "reference"
+
+    @staticmethod
+    def available() -> bool:
+        return os.path.exists(REF_SO)
+
+    def __init__(self):
+        lib = C.CDLL(REF_SO)
+        lib.ref_align.restype = C.c_int
+        lib.ref_align.argtypes = [C.c_char_p, C.c_uint, C.c_char_p, C.c_uint, C.c_int, C.c_int, C.c_int, C.c_int,
+                                  C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint), C.c_char_p, C.c_size_t,
+                                  C.POINTER(C.c_size_t), C.c_char_p, C.c_size_t]
+        lib.ref_align_batch.restype = C.c_int
+        self.lib = lib
+
+    def align(self, q: bytes, t: bytes, type: int, match: int, mismatch: int, gap: int, want_cigar=True):
+        cap = cigar_bound(len(q), len(t))
+        buf = C.create_string_buffer(cap)
+        err = C.create_string_buffer(256)
+        sc, tb, cl = C.c_int(0), C.c_uint(0), C.c_size_t(0)
+        r = self.lib.ref_align(q, len(q), t, len(t), int(type), match, mismatch, gap, int(bool(want_cigar)),
+                               C.byref(sc), C.byref(tb), buf, cap, C.byref(cl), err, 256)
+        if r:
+            raise AlignError(err.value.decode())
+        return sc.value, (buf.raw[: cl.value] if want_cigar else None), tb.value
+
+    def align_batch(self, batch, type, match, mismatch, gap, want_cigar=True, n_threads=0):
+        P = batch.n_pairs
+        off, cap, arena = self._slots(batch)
+        sc = np.zeros(P, np.int32)
+        tb = np.zeros(P, np.uint32)
+        cl = np.zeros(P, np.uint32)
+        st = np.zeros(P, np.int32)
+        self.lib.ref_align_batch(
+            C.c_uint(P), _ptr(batch.qbytes, C.c_char), _ptr(batch.qoff, C.c_uint64), _ptr(batch.qlen, C.c_uint32),
+            _ptr(batch.tbytes, C.c_char), _ptr(batch.toff, C.c_uint64), _ptr(batch.tlen, C.c_uint32),
+            C.c_int(int(type)), C.c_int(match), C.c_int(mismatch), C.c_int(gap), C.c_int(int(bool(want_cigar))),
+            C.c_int(n_threads), _ptr(sc, C.c_int32), _ptr(tb, C.c_uint32), _ptr(arena, C.c_char),
+            _ptr(off, C.c_uint64), _ptr(cap, C.c_uint64), _ptr(cl, C.c_uint32), _ptr(st, C.c_int32))
+        return BatchResult(sc, tb, cl, st, arena, off, want_cigar)
+
+
+class BatchResult:
+    def __init__(self, scores, tbs, cigar_lens, status, arena, offsets, want_cigar):
+        self.scores, self.target_begins, self.cigar_lens, self.status = scores, tbs, cigar_lens, status
+        self.arena, self.offsets, self.want_cigar = arena, offsets, want_cigar
+
+    def cigar(self, p: int) -> bytes:
+        o = int(self.offsets[p])
+        return self.arena[o : o + int(self.cigar_lens[p])].tobytes()
+
+    def cigars(self):
+        return [self.cigar(p) for p in range(len(self.scores))]

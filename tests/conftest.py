@@ -1,0 +1,72 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950); run with -m gpu on the GPU box")
+
+
+def load_cases(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)["cases"]
+
+
+def load_digest(name):
+    with open(os.path.join(GOLDEN, f"digest_{name}.json")) as f:
+        meta = json.load(f)
+    arr = np.load(os.path.join(GOLDEN, f"digest_{name}.npz"))
+    return meta, {k: arr[k] for k in arr.files}
+
+
+def digest_batch(name):
+    """Regenerate the seeded batch a digest was computed on (see make_golden.py)."""
+    from bioinfo1_amd import synth
+
+    spec = {
+        "cfg2_local": lambda: synth.uniform_batch(10000, 1000, 1000, 0x5EED),
+        "cfg2_related_local": lambda: synth.related_batch(10000, 1000, 1000, 0x5EED),
+        "g1k_global": lambda: synth.related_batch(1000, 1000, 1000, 0xA11CE),
+        "s1k_semi": lambda: synth.related_batch(1000, 1000, 1000, 0xB0B),
+        "ragged_local": lambda: synth.ragged_batch(2000, 0, 3000, 0xC0FFEE),
+        "ragged_semi": lambda: synth.ragged_batch(2000, 0, 3000, 0xD00D),
+        "ragged_global": lambda: synth.ragged_batch(2000, 0, 3000, 0xF00D),
+        "cfg5_semi_sample": lambda: synth.related_batch(32, 10000, 10000, 0x5EED),
+    }
+    return spec[name]()
+
+
+DIGESTS = ["cfg2_local", "cfg2_related_local", "g1k_global", "s1k_semi", "ragged_local", "ragged_semi",
+           "ragged_global", "cfg5_semi_sample"]
+
+
+def cigar_digest(res, P):
+    """(sha256 over length-prefixed CIGARs, per-pair crc32) -- as make_golden.py."""
+    import hashlib
+    import zlib
+
+    h = hashlib.sha256()
+    crc = np.zeros(P, np.uint32)
+    for p in range(P):
+        c = res.cigar(p)
+        h.update(len(c).to_bytes(4, "little"))
+        h.update(c)
+        crc[p] = zlib.crc32(c)
+    return h.hexdigest(), crc
+
+
+@pytest.fixture(scope="session")
+def kat_cases():
+    return load_cases("kat.json")
+
+
+@pytest.fixture(scope="session")
+def random_cases():
+    return load_cases("random_pairs.json")

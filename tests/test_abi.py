@@ -1,0 +1,62 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares
+(no compute calls: this runs without a GPU)."""
+import os
+import re
+import subprocess
+
+import pytest
+from conftest import ROOT
+
+from bioinfo1_amd import align as A
+
+HDR = os.path.join(ROOT, "include", "team_align_c.h")
+
+
+def _declared():
+    txt = open(HDR).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(ta_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_declarations_match_binding_list():
+    assert _declared() == sorted(A.ABI_SYMBOLS)
+
+
+def test_library_loads_and_exports_everything():
+    L = A.lib()
+    for s in A.ABI_SYMBOLS:
+        assert hasattr(L, s), s
+    out = subprocess.check_output(["nm", "-D", "--defined-only", A.LIB_PATH], text=True)
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    for s in A.ABI_SYMBOLS + [A.TEAM_ALIGN_SYMBOL]:
+        assert s in exported, s
+
+
+def test_team_align_symbol_matches_reference_header():
+    """Compile a caller against include/team_alignment.hpp with g++ and check
+    that the symbol it references is the one the library exports."""
+    src = ('#include "team_alignment.hpp"\n'
+           'int f(std::string* c, unsigned* t){ return team::Align("A",1,"A",1,team::AlignmentType::local,1,-1,-1,c,t);}\n')
+    tmp = os.path.join(ROOT, "build", "abi_probe")
+    os.makedirs(tmp, exist_ok=True)
+    with open(os.path.join(tmp, "probe.cpp"), "w") as f:
+        f.write(src)
+    obj = os.path.join(tmp, "probe.o")
+    subprocess.check_call(["g++", "-std=c++17", "-c", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(tmp, "probe.cpp"), "-o", obj])
+    und = subprocess.check_output(["nm", "-u", obj], text=True)
+    assert A.TEAM_ALIGN_SYMBOL in und
+
+
+def test_status_strings_mirror_reference_messages():
+    L = A.lib()
+    assert L.ta_status_string(A.TA_ERR_BAD_TYPE) == b"Unknown AlignmentType provided."
+    assert L.ta_status_string(A.TA_ERR_CIGAR) == b"Unknown error in determining cigar string."
+    assert L.ta_cigar_slot_bytes(0, 0) == 2 and L.ta_cigar_slot_bytes(1000, 1000) == 4002
+
+
+@pytest.mark.parametrize("bad", [3, -1, 7])
+def test_bad_type_raises_like_reference(bad):
+    # validated on the host before any device work, as Align's first switch (:58-74)
+    with pytest.raises(ValueError, match=r"Unknown AlignmentType provided\."):
+        A.align(b"ACGT", b"ACGT", bad, 1, -1, -1)

@@ -1,0 +1,161 @@
+"""GPU parity: the gfx950 kernels (through the C-ABI) against the committed
+golden vectors (made by the reference itself) and against the CPU oracle on
+seeded batches.  Bit-exact: scores, target_begin and CIGAR bytes."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+from conftest import DIGESTS, ROOT, cigar_digest, digest_batch, load_digest
+
+from bioinfo1_amd import synth
+from bioinfo1_amd.align import Aligner, DevicePlan, align
+from oracle.pyoracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def aligner():
+    return Aligner(0)
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return Oracle()
+
+
+def _run_cases(aligner, cases):
+    groups = {}
+    for c in cases:
+        groups.setdefault((c["type"], c["match"], c["mismatch"], c["gap"]), []).append(c)
+    n = 0
+    for (typ, m, mm, g), cs in groups.items():
+        if cs[0]["error"]:
+            for c in cs:
+                with pytest.raises(ValueError, match=r"Unknown AlignmentType provided\."):
+                    align(bytes.fromhex(c["query"]), bytes.fromhex(c["target"]), typ, m, mm, g)
+            continue
+        b = synth.from_pairs([(bytes.fromhex(c["query"]), bytes.fromhex(c["target"])) for c in cs])
+        r = aligner.align_batch(b, typ, m, mm, g, True)
+        r0 = aligner.align_batch(b, typ, m, mm, g, False)
+        for k, c in enumerate(cs):
+            got = (int(r.scores[k]), r.cigar(k), int(r.target_begins[k]))
+            assert got == (c["score"], bytes.fromhex(c["cigar"]), c["target_begin"]), (c["source"], c, got)
+            assert (int(r0.scores[k]), int(r0.target_begins[k])) == (c["score"], c["target_begin"])
+            n += 1
+    return n
+
+
+def test_kat(aligner, kat_cases):
+    assert _run_cases(aligner, kat_cases) > 300
+
+
+def test_random_pairs(aligner, random_cases):
+    assert _run_cases(aligner, random_cases) == 300
+
+
+def test_config1_single_call():
+    # BASELINE config 1 through the single-pair mirror of team::Align
+    assert align(b"GTACC", b"GATACGTTA", 0, 1, -1, -1) == (-1, b"1M1I3M3I1M", 0)
+
+
+@pytest.mark.parametrize("name", DIGESTS)
+def test_digest(aligner, name):
+    meta, d = load_digest(name)
+    batch = digest_batch(name)
+    r = aligner.align_batch(batch, meta["type"], meta["match"], meta["mismatch"], meta["gap"], True)
+    np.testing.assert_array_equal(r.scores, d["scores"])
+    np.testing.assert_array_equal(r.target_begins, d["target_begins"])
+    np.testing.assert_array_equal(r.cigar_lens, d["cigar_lens"])
+    sha, crc = cigar_digest(r, batch.n_pairs)
+    np.testing.assert_array_equal(crc, d["cigar_crc32"])
+    assert sha == meta["cigar_sha256"]
+    r0 = aligner.align_batch(batch, meta["type"], meta["match"], meta["mismatch"], meta["gap"], False)
+    np.testing.assert_array_equal(r0.scores, d["scores"])
+    np.testing.assert_array_equal(r0.target_begins, d["target_begins"])
+
+
+FUZZ = [
+    # (mode, scoring, alphabet, min_len, max_len, n_pairs)
+    (0, (1, -1, -1), b"ACGT", 0, 80, 400),
+    (1, (1, -1, -1), b"ACGT", 0, 80, 400),
+    (2, (1, -1, -1), b"ACGT", 0, 80, 400),
+    (0, (2, -1, 2), b"AC-GT", 0, 300, 200),
+    (1, (2, -1, 2), b"AC-GT", 0, 300, 200),
+    (2, (3, -2, 0), b"acgtN-", 0, 300, 200),
+    (1, (5, 4, -1), b"AC", 900, 1200, 40),
+    (2, (1, -1, -1), b"ACGT", 1000, 1100, 40),
+    (0, (1, 2, -3), b"ACGT", 1020, 1030, 40),
+    (1, (1, -1, -1), b"ACGT", 2040, 2060, 16),
+    (2, (2, -3, -1), b"ACGT-", 2040, 2060, 16),
+    (0, (1, -1, -1), b"ACGT", 3000, 3100, 8),
+    (1, (100000, -70000, -90000), b"ACGT", 0, 1500, 60),  # unpacked (WIDE) local argmax
+    (1, (40000, -1, -1), b"AC", 1500, 2100, 12),           # WIDE + multi-pass
+]
+
+
+@pytest.mark.parametrize("case", range(len(FUZZ)))
+def test_oracle_fuzz(aligner, oracle, case):
+    mode, sc, alpha, lo, hi, P = FUZZ[case]
+    b = synth.ragged_batch(P, lo, hi, seed=0xF022 + case, alphabet=alpha)
+    want = oracle.align_batch(b, mode, *sc, True)
+    got = aligner.align_batch(b, mode, *sc, True)
+    for p in range(P):
+        assert (int(got.scores[p]), got.cigar(p), int(got.target_begins[p])) == (
+            int(want.scores[p]), want.cigar(p), int(want.target_begins[p])), (case, p, b.qlen[p], b.tlen[p])
+
+
+def test_related_long_pairs(aligner, oracle):
+    # long tracebacks across pass and tile boundaries
+    for mode in (0, 1, 2):
+        b = synth.related_batch(6, 2500, 2600, seed=77 + mode)
+        want = oracle.align_batch(b, mode, 1, -1, -1, True)
+        got = aligner.align_batch(b, mode, 1, -1, -1, True)
+        assert want.cigars() == got.cigars()
+        np.testing.assert_array_equal(want.scores, got.scores)
+
+
+def test_device_plan_and_chunking(aligner):
+    import torch
+
+    b = synth.uniform_batch(300, 1000, 1000, seed=11)
+    host = aligner.align_batch(b, 1, 1, -1, -1, True)
+    for budget in (0, 3 * 1063 * 256):  # default, and ~3 pairs per chunk
+        plan = DevicePlan(aligner, b, 1, 1, -1, -1, True, workspace_budget=budget)
+        assert plan.chunks == (1 if budget == 0 else 100)
+        plan.run()
+        torch.cuda.synchronize()
+        r = plan.results()
+        np.testing.assert_array_equal(r.scores, host.scores)
+        np.testing.assert_array_equal(r.target_begins, host.target_begins)
+        assert r.cigars() == host.cigars()
+        plan.close()
+
+
+def _shim_binary():
+    out = os.path.join(ROOT, "build", "shim_caller")
+    libdir = os.path.join(ROOT, "bioinfo1_amd")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-pthread", "-I", os.path.join(ROOT, "include"),
+                           os.path.join(ROOT, "tests", "cpp", "shim_caller.cpp"), "-L", libdir,
+                           "-lteam_alignment", f"-Wl,-rpath,{libdir}", "-o", out])
+    return out
+
+
+def test_team_align_dropin(kat_cases, random_cases):
+    """An unmodified team::Align caller links and gets the reference's
+    answers (incl. the exception message), single- and multi-threaded."""
+    exe = _shim_binary()
+    cases = kat_cases + random_cases[:60]
+    lines = [f"{c['type']} {c['match']} {c['mismatch']} {c['gap']} {c['query'] or '-'} {c['target'] or '-'}"
+             for c in cases]
+    want = []
+    for c in cases:
+        if c["error"]:
+            want.append(f"ERR {c['error']}")
+        else:
+            want.append(f"{c['score']} {c['target_begin']} {c['cigar'] or '-'}")
+    for mode in ([], ["threads"]):
+        out = subprocess.run([exe] + mode, input="\n".join(lines) + "\n", capture_output=True, text=True,
+                             timeout=600, check=True).stdout.splitlines()
+        assert out == want

@@ -1,0 +1,78 @@
+"""The CPU oracle (oracle/align_oracle.c) is pinned to the reference:
+every golden vector in tests/golden/ was produced by the unmodified reference
+team_alignment.cpp (tests/golden/make_golden.py), and the restatement must
+reproduce all of them bit for bit -- scores, CIGAR bytes (incl. the "1\\0"
+empty case), target_begin and the two error messages."""
+import numpy as np
+import pytest
+from conftest import DIGESTS, cigar_digest, digest_batch, load_digest
+
+from oracle.pyoracle import AlignError, Oracle, Reference
+
+
+@pytest.fixture(scope="module")
+def oracle():
+    return Oracle()
+
+
+def _check_case(o, c):
+    q, t = bytes.fromhex(c["query"]), bytes.fromhex(c["target"])
+    args = (q, t, c["type"], c["match"], c["mismatch"], c["gap"])
+    if c["error"]:
+        with pytest.raises(AlignError, match=c["error"].replace(".", r"\.")):
+            o.align(*args)
+        return
+    s, cig, tb = o.align(*args, want_cigar=True)
+    assert (s, cig, tb) == (c["score"], bytes.fromhex(c["cigar"]), c["target_begin"]), c["source"]
+    s2, cig2, tb2 = o.align(*args, want_cigar=False)
+    assert (s2, cig2, tb2) == (c["score"], None, c["target_begin"])
+
+
+def test_kat(oracle, kat_cases):
+    assert len(kat_cases) > 300
+    for c in kat_cases:
+        _check_case(oracle, c)
+
+
+def test_doc_kats_present(kat_cases):
+    docs = [c for c in kat_cases if "doc_expect" in c]
+    assert len(docs) == 6
+    assert any(c["source"] == "BASELINE config 1" and c["score"] == -1 and bytes.fromhex(c["cigar"]) == b"1M1I3M3I1M"
+               for c in docs)
+
+
+def test_random_pairs(oracle, random_cases):
+    assert len(random_cases) == 300
+    for c in random_cases:
+        _check_case(oracle, c)
+
+
+@pytest.mark.parametrize("name", DIGESTS)
+def test_digest(oracle, name):
+    meta, d = load_digest(name)
+    batch = digest_batch(name)
+    assert batch.n_pairs == meta["n_pairs"] and batch.cells == meta["cells"]
+    res = oracle.align_batch(batch, meta["type"], meta["match"], meta["mismatch"], meta["gap"], True)
+    assert not res.status.any()
+    np.testing.assert_array_equal(res.scores, d["scores"])
+    np.testing.assert_array_equal(res.target_begins, d["target_begins"])
+    np.testing.assert_array_equal(res.cigar_lens, d["cigar_lens"])
+    sha, crc = cigar_digest(res, batch.n_pairs)
+    np.testing.assert_array_equal(crc, d["cigar_crc32"])
+    assert sha == meta["cigar_sha256"]
+
+
+@pytest.mark.skipif(not Reference.available(), reason="oracle/_ref not built (reference sources absent)")
+def test_oracle_matches_reference_fuzz(oracle):
+    """Fresh random pairs (not in the fixtures), oracle vs compiled reference."""
+    ref = Reference()
+    rng = np.random.default_rng(1234)
+    alphas = [b"ACGT", b"AC", b"ACGT-", b"acgtN"]
+    schemes = [(1, -1, -1), (2, -3, -2), (2, -1, 2), (0, 0, 0), (4, 4, -1), (-2, -1, 1)]
+    for k in range(1500):
+        a = np.frombuffer(alphas[k % 4], np.uint8)
+        q = bytes(rng.choice(a, int(rng.integers(0, 60))))
+        t = bytes(rng.choice(a, int(rng.integers(0, 60))))
+        typ = int(rng.integers(0, 3))
+        sm = schemes[k % len(schemes)]
+        assert oracle.align(q, t, typ, *sm) == ref.align(q, t, typ, *sm), (q, t, typ, sm)
