@@ -298,7 +298,7 @@ static int check_io(ta_plan* pl, const ta_device_io* io) {
 int ta_plan_execute(ta_plan* pl, const ta_device_io* io, void* stream) {
     if (int r = check_io(pl, io)) return r;
     TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
-    hipStream_t s = stream ? (hipStream_t)stream : pl->ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     for (uint32_t c = 0; c < pl->chunks.size(); ++c)
         if (int r = exec_chunk(pl, io, s, c, true, true)) return r;
     return TA_OK;
@@ -307,14 +307,14 @@ int ta_plan_execute(ta_plan* pl, const ta_device_io* io, void* stream) {
 int ta_plan_execute_fill(ta_plan* pl, const ta_device_io* io, void* stream, uint32_t chunk) {
     if (int r = check_io(pl, io)) return r;
     if (chunk >= pl->chunks.size()) return pl->n_pairs ? TA_ERR_ARG : TA_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : pl->ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     return exec_chunk(pl, io, s, chunk, true, false);
 }
 
 int ta_plan_execute_traceback(ta_plan* pl, const ta_device_io* io, void* stream, uint32_t chunk) {
     if (int r = check_io(pl, io)) return r;
     if (chunk >= pl->chunks.size()) return pl->n_pairs ? TA_ERR_ARG : TA_OK;
-    hipStream_t s = stream ? (hipStream_t)stream : pl->ctx->stream;
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
     return exec_chunk(pl, io, s, chunk, false, true);
 }
 

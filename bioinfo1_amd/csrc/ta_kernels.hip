@@ -312,7 +312,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
             o.row_j = (uint32_t)rdlane((int)rowbest_j, nl - 1);
         }
     } else {
-        if (last_pass) o.corner = rdlane(select_row<R>(H, NV - 1), nl - 1);
+        if (last_pass) o.corner = rdlane(select_row<R>(H, nrows - (nl - 1) * R - 1), nl - 1);  // row n
     }
     return o;
 }

@@ -108,8 +108,8 @@ typedef struct ta_device_io {
     uint32_t* cigar_len;          /* device, n_pairs */
 } ta_device_io;
 
-/* Enqueue the whole batch on `hip_stream` (a hipStream_t; NULL = the
- * context's stream).  Asynchronous: returns after enqueueing. */
+/* Enqueue the whole batch on `hip_stream` (a hipStream_t; NULL = the HIP
+ * null stream, as everywhere in HIP).  Asynchronous: returns after enqueueing. */
 int ta_plan_execute(ta_plan* plan, const ta_device_io* io, void* hip_stream);
 
 /* Enqueue only the DP fill (scores/target_begin; traceback pointers into the

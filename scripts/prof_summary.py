@@ -1,0 +1,81 @@
+#!/usr/bin/env python3
+"""Summarise a scripts/profile.sh run into profiles/<round>_*.
+
+  python scripts/prof_summary.py gpurun_out/<tag> <round-tag> <workload-tag>
+
+Writes profiles/<round-tag>_kernel_stats.csv (the rocprofv3 --stats summary),
+profiles/<round-tag>_pmc.json (per-kernel average counters per dispatch) and
+merges per-launch HBM traffic of the fill kernel into profiles/traffic.json
+and VALU instructions per DP cell into profiles/valu.json (read by bench.py).
+
+HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come
+from separate passes; FETCH_SIZE is reported in KB and reads 1/2 of the bytes
+of wide coalesced streaming reads on gfx950, so it is doubled; WRITE_SIZE (KB)
+is taken as is."""
+import csv
+import glob
+import json
+import os
+import shutil
+import sys
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def find(d, pat):
+    r = glob.glob(os.path.join(d, "**", pat), recursive=True)
+    return r[0] if r else None
+
+
+def pmc_avgs(d):
+    f = find(d, "*counter_collection.csv")
+    if not f:
+        return {}
+    acc = defaultdict(lambda: defaultdict(list))
+    with open(f) as fh:
+        for row in csv.DictReader(fh):
+            k = row.get("Kernel_Name", "?")
+            acc[k][row["Counter_Name"]].append(float(row["Counter_Value"]))
+    return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
+
+
+def main():
+    src, rtag, wtag = sys.argv[1], sys.argv[2], sys.argv[3]
+    prof = os.path.join(ROOT, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    st = find(os.path.join(src, "prof_trace"), "*kernel_stats.csv")
+    if st:
+        shutil.copy(st, os.path.join(prof, f"{rtag}_kernel_stats.csv"))
+    pmc = {}
+    for part in ("prof_fetch", "prof_write", "prof_sq", "prof_busy"):
+        for k, cs in pmc_avgs(os.path.join(src, part)).items():
+            pmc.setdefault(k, {}).update(cs)
+    with open(os.path.join(prof, f"{rtag}_pmc.json"), "w") as fh:
+        json.dump(pmc, fh, indent=1)
+    fill = {k: v for k, v in pmc.items() if "fill_kernel" in k}
+    if fill:
+        k, cs = next(iter(fill.items()))
+        tr = None
+        if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
+            tr = int((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024)
+        p = os.path.join(prof, "traffic.json")
+        d = json.load(open(p)) if os.path.exists(p) else {}
+        d[wtag] = tr
+        json.dump(d, open(p, "w"), indent=1)
+        if "SQ_INSTS_VALU" in cs:
+            # SQ_INSTS_VALU counts wave-instructions; cells per launch from the workload tag
+            parts = wtag.split("_")[-1].split("x")
+            cells = int(parts[0]) * int(parts[1]) * int(parts[2])
+            waves = cs.get("SQ_WAVES", 0)
+            # per lane-cell: wave-instr x 64 lanes / cells
+            p = os.path.join(prof, "valu.json")
+            d = json.load(open(p)) if os.path.exists(p) else {}
+            d[wtag] = round(cs["SQ_INSTS_VALU"] * 64 / cells, 3)
+            json.dump(d, open(p, "w"), indent=1)
+        print(k, json.dumps(cs, indent=1))
+    print("summary written to", prof)
+
+
+if __name__ == "__main__":
+    main()
