@@ -163,13 +163,13 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     pl->want_cigar = want_cigar != 0;
     pl->qlen.assign(qlen, qlen + n_pairs);
     pl->tlen.assign(tlen, tlen + n_pairs);
-    // Local mode packs (score << 5 | row) into 32 bits; take the unpacked
-    // argmax when any local score could reach 2^26.
+    // Local mode keeps V = 32*score + row tag in int32; take the unscaled
+    // ("wide") kernel when any local value could reach 2^25 in magnitude.
     uint64_t maxlen = 0;
     for (uint32_t p = 0; p < n_pairs; ++p) maxlen = std::max<uint64_t>(maxlen, (uint64_t)qlen[p] + tlen[p]);
     const uint64_t mag = std::max<uint64_t>({1ull, (uint64_t)std::llabs(match), (uint64_t)std::llabs(mismatch),
                                              (uint64_t)std::llabs(gap)});
-    pl->wide = (type == TA_LOCAL) && (maxlen * mag >= (1ull << 26));
+    pl->wide = (type == TA_LOCAL) && (maxlen * mag >= (1ull << 25));
     // Longest pairs first (fewer stragglers), stable for equal cell counts.
     pl->order.resize(n_pairs);
     std::iota(pl->order.begin(), pl->order.end(), 0u);

@@ -80,9 +80,11 @@ struct CompactArgs {
     char* dst;
 };
 
-// Launchers (ta_kernels.hip).  `wide` selects the local-mode argmax that does
-// not pack (score,row) into one 32-bit key (needed only for |scores| >= 2^26).
+// Launchers (ta_kernels.hip).  `wide` selects the unscaled local-mode kernel
+// (needed only when |scores| could reach 2^25; see run_pass SCALED).
 hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s);
+template <int MODE, bool CIGAR>
+hipError_t launch_fill_mode(bool wide, const FillArgs& a, hipStream_t s);
 hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 

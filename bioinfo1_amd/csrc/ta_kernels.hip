@@ -91,6 +91,7 @@ __device__ __forceinline__ int load_bchunk(const int32_t* B, uint32_t m, uint32_
     return j <= m ? B[j] : 0;
 }
 
+#ifdef TA_FILL_MODE
 // Degenerate pairs (an empty query or target): closed forms of what the
 // reference computes when one of its loops is empty.
 template <int MODE>
@@ -132,36 +133,80 @@ struct PassOut {
     int corner;      // global, last pass: H[n][m]
 };
 
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+template <int C>
+__device__ __forceinline__ int max3_imm(int a, int b) {
+    // max(a, b, C) with C an inline constant.  Kept opaque so that hipcc does
+    // not split it back into two v_max when a later compare reads the result
+    // (it rewrites h == C into max(a,b) <= C).
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "i"(C));
+    return r;
+}
+
 // One pass = rows row_base+1 .. row_base+nrows of the query against the whole
-// target.  NV = valid rows of the last lane in use (compile-time, so every
-// register index below is static).
-template <int MODE, bool CIGAR, bool WIDE, int NV>
+// target.  Compile-time specialisation:
+//   NV     valid rows of the last lane in use (every register index static);
+//   QDASH  some query row of this pass is '-' (free vertical gap): the per-row
+//          gap is then recomputed per cell, otherwise it is the uniform `gap`;
+//   SCALED (local, |scores| < 2^25): each register holds V = 32*H + c_r with
+//          c_r = 16 - r.  The recurrence is unchanged up to per-row offsets
+//          folded into the constants (diag/up gain -1 per row, +15 into row 0
+//          from the lane above's row 15), the clamp becomes max(.., c_r), and
+//          V itself is the argmax key: larger H first, then the smaller row.
+template <int MODE, bool CIGAR, bool WIDE, int NV, bool QDASH>
 __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
                                             uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
                                             int32_t* B, int lane) {
     constexpr int R = kRows;
-    const int ma = a.match, mi = a.mismatch, gap = a.gap;
-    const int init = (MODE == kGlobal) ? gap : 0;  // :58-74
+    constexpr bool SCALED = (MODE == kLocal) && !WIDE;
+    constexpr int SC = SCALED ? 32 : 1;
+    const int gap = a.gap;
+    // score constants for rows >= 1 (row 0 gets +16 on diag and up when SCALED)
+    const int MA = SC * a.match - (SCALED ? 1 : 0);
+    const int MI = SC * a.mismatch - (SCALED ? 1 : 0);
+    const int UPG = SC * gap - (SCALED ? 1 : 0);   // up gain, query char != '-'
+    const int UPD = SCALED ? -1 : 0;                 // up gain, query char == '-'
+    const int GTG = SC * gap;                        // left gain, target char != '-'
+    const int init = (MODE == kGlobal) ? gap : 0;    // :58-74 (local/semi boundaries are 0)
     const uint32_t Tmax = pass_steps(m);
     const uint32_t row_base = pass * kPassRows;
     const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
     const uint32_t nl = (nrows + R - 1) / R;  // lanes in use; lane nl-1 holds NV valid rows
     const bool has_next = !last_pass;
 
-    int qc[R], gq[R], H[R];
+    uint32_t qp[R / 4];  // the lane's 16 query bytes, 4 per register (compared with SDWA byte selects)
+    int H[R];
+#pragma unroll
+    for (int k = 0; k < R / 4; ++k) {
+        uint32_t w = 0;
+#pragma unroll
+        for (int b = 0; b < 4; ++b) {
+            const uint32_t i0 = row_base + (uint32_t)lane * R + 4 * k + b;
+            w |= (i0 < n ? (uint32_t)Q[i0] : 0u) << (8 * b);
+        }
+        qp[k] = w;
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-        const uint32_t i0 = row_base + (uint32_t)lane * R + r;  // query index of row i0+1
-        qc[r] = i0 < n ? (int)Q[i0] : 0x100;                    // 0x100 never equals a byte
-        gq[r] = (qc[r] == '-') ? 0 : gap;                       // indel(q[i-1]) :25-28
-        H[r] = wmul(i0 + 1, init);                               // column 0, :83-86
+        const uint32_t i0 = row_base + (uint32_t)lane * R + r;  // row i0+1
+        H[r] = SCALED ? (R - r) : wmul(i0 + 1, init);           // column 0, :83-86
     }
-    int recv = wmul(row_base + (uint32_t)lane * R, init);  // H[row above the stripe][0]
-    int tc = 0x100;
+    int recv = SCALED ? 1 : wmul(row_base + (uint32_t)lane * R, init);  // H[row above the stripe][0]
+    int tc = 0;
     const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
 
-    uint32_t bestkey = 0, bestj = 0;  // local: key = h<<5 | (16-r)
-    int bh = INT_MIN;                 // local, WIDE: unpacked (h, r, j)
+    int bestkey = 0;                  // local SCALED: best V (0 = none: every real V >= 1)
+    uint32_t bestj = 0;
+    int bh = INT_MIN;                 // local WIDE: unpacked (h, r, j)
     uint32_t br = 0, bj = 0;
     int rowbest = INT_MIN;            // semi: row n
     uint32_t rowbest_j = 0;
@@ -173,7 +218,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
         bnext = load_bchunk(B, m, 1, lane);
     }
     const uint32_t steps = m + nl - 1;
-    const uint64_t step_base = (uint64_t)pass * Tmax;
+    uint32_t* prow = CIGAR ? ptrs + (uint64_t)pass * Tmax * kWave : nullptr;
 
     // One step = one target column per lane (lane l at column t-l+1).
     // MASKED steps (the ramp-up / ramp-down of the lane skew) run the cell
@@ -188,7 +233,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
         }
         int top;
         if (pass == 0) {
-            top = wmul(t + 1, init);  // row 0, :89-92
+            top = SCALED ? 1 : wmul(t + 1, init);  // row 0, :89-92
         } else {
             if ((t & 63u) == 0 && t) {
                 bcur = bnext;
@@ -206,18 +251,31 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
         uint32_t acc = 0;
         if (active) {
-            const int gt = (tc == '-') ? 0 : gap;  // indel(t[j-1])
-            int dg = prev, upv = recv;
+            const int gt = (tc == '-') ? 0 : GTG;  // indel(t[j-1])
 #pragma unroll
-            for (int r = 0; r < R; ++r) {
+            for (int k = 0; k < R / 4; ++k) asm volatile("" : "+v"(qp[k]));  // keep bytes packed (SDWA compares)
+            // match_func :20-23 for row r against this column's target byte
+            auto score_of = [&](int r) {
+                const uint32_t qb = (qp[r >> 2] >> (8 * (r & 3))) & 0xFFu;
+                return (qb == (uint32_t)tc) ? MA : MI;
+            };
+            // diag of the next row is formed from old H[r] before h_r is
+            // written, so h_r can take H[r]'s register (no rotation copies)
+            int dnext = wadd(SCALED ? wadd(prev, 16) : prev, score_of(0));
+            int upv = SCALED ? wadd(recv, 16) : recv;
+            static_for<0, R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
                 const int old = H[r];
-                const int s = (qc[r] == tc) ? ma : mi;  // match_func :20-23
-                const int diag = wadd(dg, s);
+                const int diag = dnext;
                 const int left = wadd(old, gt);
-                const int up = wadd(upv, gq[r]);
+                if constexpr (r + 1 < R) dnext = wadd(old, score_of(r + 1));
+                int upg = UPG;  // indel(q[i-1])
+                if (QDASH) upg = (((qp[r >> 2] >> (8 * (r & 3))) & 0xFFu) == (uint32_t)'-') ? UPD : UPG;
+                const int up = wadd(upv, upg);
                 const int m1 = max(diag, left);
-                int h = max(m1, up);
-                if (MODE == kLocal) h = max(h, 0);  // :185
+                int h;
+                if (MODE == kLocal) h = SCALED ? max3_imm<R - r>(m1, up) : max3_imm<0>(m1, up);  // clamp, :185
+                else h = max(m1, up);
                 if (CIGAR) {
                     // wave-wide lane masks from the VALU compares; the
                     // canonical code is formed on the SALU:
@@ -226,7 +284,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
                     const uint64_t mI = ballot(left > diag);  // INSERT beats MATCH only if strictly greater
                     uint64_t hi = mD, lo = mI & ~mD;
                     if (MODE == kLocal) {
-                        const uint64_t mS = ballot(h == 0);   // cost 0 ends the local walk
+                        const uint64_t mS = ballot(h == (SCALED ? (R - r) : 0));  // cost 0 ends the walk
                         hi |= mS;
                         lo |= mS;
                     }
@@ -241,19 +299,17 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
                     }
                 }
                 H[r] = h;
-                dg = old;
                 upv = h;
-            }
-            if (MODE == kLocal && !WIDE) {
-                // key = h*32 + (16-r): larger score first, then the smaller row;
-                // strict '>' over steps keeps the first column (:186).
-                uint32_t P[R];
-                P[0] = ((uint32_t)H[0] << 5) | (uint32_t)R;
+            });
+            if (SCALED) {
+                // step key = max V over the lane's valid rows (prefix max chain)
+                int P[R];
+                P[0] = H[0];
 #pragma unroll
-                for (int r = 1; r < R; ++r) P[r] = max(P[r - 1], ((uint32_t)H[r] << 5) | (uint32_t)(R - r));
-                uint32_t sk = P[R - 1];
+                for (int r = 1; r < R; ++r) P[r] = max(P[r - 1], H[r]);
+                int sk = P[R - 1];
                 if (NV != R) sk = ((uint32_t)lane == nl - 1) ? P[NV - 1] : sk;
-                if (sk > bestkey) {
+                if (sk > bestkey) {  // strict: the first column keeps a tie (:186)
                     bestkey = sk;
                     bestj = (uint32_t)j;
                 }
@@ -267,7 +323,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
             }
             if (has_next && (uint32_t)lane == nl - 1) B[j] = H[R - 1];
         }
-        if (CIGAR) ptrs[(step_base + t) * kWave + lane] = acc;
+        if (CIGAR) prow[t * kWave + lane] = acc;
     };
     // lanes 0..nl-1 are all active for t in [nl-1, m-1]
     const uint32_t ramp_end = min(nl - 1, steps);
@@ -278,12 +334,12 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
 
     PassOut o{INT_MIN, 0, 0, INT_MIN, 0, 0};
     if (MODE == kLocal) {
-        const int v = (uint32_t)lane >= nl ? INT_MIN : (WIDE ? bh : (bestkey ? (int)(bestkey >> 5) : -1));
+        const int v = (uint32_t)lane >= nl ? INT_MIN : (WIDE ? bh : (bestkey ? (bestkey >> 5) : -1));
         const int mx = wave_max(v);
         const int fl = first_lane(v == mx);
         uint32_t r, j;
         if (!WIDE) {
-            r = R - ((uint32_t)rdlane((int)bestkey, fl) & 31u);
+            r = R - ((uint32_t)rdlane(bestkey, fl) & 31u);
             j = (uint32_t)rdlane((int)bestj, fl);
         } else {
             r = (uint32_t)rdlane((int)br, fl);
@@ -317,23 +373,40 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
     return o;
 }
 
-template <int MODE, bool CIGAR, bool WIDE>
+template <int MODE, bool CIGAR, bool WIDE, bool QDASH>
 __device__ __forceinline__ PassOut run_pass_nv(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
-                                            uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
-                                            int32_t* B, int lane) {
+                                               uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
+                                               int32_t* B, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
-    // Global needs NV only for the corner cell, which run_pass reads with a
-    // runtime select; local/semi specialise the step loop on NV.
-    if (MODE == kGlobal || nv == kRows) return run_pass<MODE, CIGAR, WIDE, kRows>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
+    // Global needs NV only for the corner cell (read with a runtime select);
+    // local/semi specialise the step loop on NV.
+    // (WIDE tracks the argmax per row with a runtime row bound: no NV needed)
+    if (MODE == kGlobal || (MODE == kLocal && WIDE) || nv == kRows)
+        return run_pass<MODE, CIGAR, WIDE, kRows, QDASH>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
 #define TA_NV_CASE(k) \
-    case k: return run_pass<MODE, CIGAR, WIDE, k>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
+    case k: return run_pass<MODE, CIGAR, WIDE, k, QDASH>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
         default: TA_NV_CASE(15)
     }
 #undef TA_NV_CASE
+}
+
+template <int MODE, bool CIGAR, bool WIDE>
+__device__ __forceinline__ PassOut run_pass_any(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
+                                                uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
+                                                int32_t* B, int lane) {
+    // does any query row of this pass hold '-' (free vertical gap)?
+    bool dash = false;
+    const uint32_t row0 = pass * kPassRows + (uint32_t)lane * kRows;
+#pragma unroll
+    for (int r = 0; r < kRows; ++r) dash |= (row0 + r < n) && Q[row0 + r] == '-';
+#ifndef TA_ANALYSIS_NODASH  // analysis builds: drop the dash variant to read the common loop
+    if (__ballot(dash)) return run_pass_nv<MODE, CIGAR, WIDE, true>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
+#endif
+    return run_pass_nv<MODE, CIGAR, WIDE, false>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
 }
 
 template <int MODE, bool CIGAR, bool WIDE>
@@ -359,7 +432,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
     int corner = 0;
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const bool last_pass = pass + 1 == passes;
-        const PassOut o = run_pass_nv<MODE, CIGAR, WIDE>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
+        const PassOut o = run_pass_any<MODE, CIGAR, WIDE>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
         if (MODE != kGlobal && o.h > best_h) {  // strict: the earlier (upper) pass wins ties
             best_h = o.h;
             best_i = o.i;
@@ -382,6 +455,9 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
     }
 }
 
+#endif  // TA_FILL_MODE
+
+#ifdef TA_TU_MISC
 // ---------------------------------------------------------------------------
 // Traceback: one wave per pair, the walk itself is wave-uniform (SALU); the
 // wave's lanes only fetch 64-step x 4-lane tiles of the pointer matrix
@@ -503,30 +579,39 @@ __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
     for (uint32_t k = (uint32_t)lane; k < len; k += 64u) dst[k] = src[k];
 }
 
-inline dim3 grid_for(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock); }
+#endif  // TA_TU_MISC
 
-template <int MODE>
-hipError_t launch_fill_mode(bool cigar, bool wide, const FillArgs& a, hipStream_t s) {
-    if (!a.count) return hipSuccess;
-    const dim3 g = grid_for(a.count), b(kBlock);
-    if (cigar) {
-        if (wide) hipLaunchKernelGGL((fill_kernel<MODE, true, true>), g, b, 0, s, a);
-        else hipLaunchKernelGGL((fill_kernel<MODE, true, false>), g, b, 0, s, a);
-    } else {
-        if (wide) hipLaunchKernelGGL((fill_kernel<MODE, false, true>), g, b, 0, s, a);
-        else hipLaunchKernelGGL((fill_kernel<MODE, false, false>), g, b, 0, s, a);
-    }
-    return hipGetLastError();
-}
+inline dim3 grid_for(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock); }
 
 }  // namespace
 
-hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s) {
+// Each fill mode is its own translation unit (build.sh compiles this file
+// once per TA_FILL_MODE in parallel); TA_TU_MISC holds the rest.
+#ifdef TA_FILL_MODE
+// One translation unit per (mode, cigar) pair: build.sh compiles this file
+// six times in parallel with -DTA_FILL_MODE=m -DTA_FILL_CIGAR=c.
+template <>
+hipError_t launch_fill_mode<TA_FILL_MODE, (TA_FILL_CIGAR != 0)>(bool wide, const FillArgs& a, hipStream_t s) {
+    constexpr int MODE = TA_FILL_MODE;
+    constexpr bool CIGAR = TA_FILL_CIGAR != 0;
+    if (!a.count) return hipSuccess;
+    const dim3 g = grid_for(a.count), b(kBlock);
     // WIDE only changes the local argmax; other modes use one instantiation.
-    switch (mode) {
-        case kGlobal: return launch_fill_mode<kGlobal>(cigar, false, a, s);
-        case kLocal: return launch_fill_mode<kLocal>(cigar, wide, a, s);
-        case kSemi: return launch_fill_mode<kSemi>(cigar, false, a, s);
+    if (MODE == kLocal && wide) hipLaunchKernelGGL((fill_kernel<MODE, CIGAR, MODE == kLocal>), g, b, 0, s, a);
+    else hipLaunchKernelGGL((fill_kernel<MODE, CIGAR, false>), g, b, 0, s, a);
+    return hipGetLastError();
+}
+#endif
+
+#ifdef TA_TU_MISC
+hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s) {
+    switch (mode * 2 + (cigar ? 1 : 0)) {
+        case 0: return launch_fill_mode<kGlobal, false>(wide, a, s);
+        case 1: return launch_fill_mode<kGlobal, true>(wide, a, s);
+        case 2: return launch_fill_mode<kLocal, false>(wide, a, s);
+        case 3: return launch_fill_mode<kLocal, true>(wide, a, s);
+        case 4: return launch_fill_mode<kSemi, false>(wide, a, s);
+        case 5: return launch_fill_mode<kSemi, true>(wide, a, s);
         default: return hipErrorInvalidValue;
     }
 }
@@ -548,5 +633,6 @@ hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
     hipLaunchKernelGGL(compact_kernel, grid_for(a.n_pairs), dim3(kBlock), 0, s, a);
     return hipGetLastError();
 }
+#endif
 
 }  // namespace ta

@@ -1,17 +1,27 @@
 #!/usr/bin/env bash
 # Builds libteam_alignment.so (gfx950 HIP kernels + C-ABI + team::Align shim)
 # in-tree, and the test-only oracle libraries.  Used by __graft_entry__.build().
+# ta_kernels.hip is compiled once per (fill mode, cigar) pair (TA_FILL_MODE,
+# TA_FILL_CIGAR) and once for the traceback/compact kernels (TA_TU_MISC), in
+# parallel.
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")" && pwd)"
 CS="$ROOT/bioinfo1_amd/csrc"
 OUT="$ROOT/bioinfo1_amd/libteam_alignment.so"
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
-mkdir -p "$ROOT/build"
-FLAGS=(-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result)
-"$HIPCC" "${FLAGS[@]}" -c "$CS/ta_kernels.hip" -o "$ROOT/build/ta_kernels.o" &
-"$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip" -o "$ROOT/build/ta_api.o" &
-"$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp" -o "$ROOT/build/shim.o" &
-wait %1 && wait %2 && wait %3
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$ROOT/build/ta_kernels.o" "$ROOT/build/ta_api.o" "$ROOT/build/shim.o" -o "$OUT"
+B="$ROOT/build"
+mkdir -p "$B"
+FLAGS=(-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-unused-function ${TA_EXTRA_FLAGS:-})
+pids=()
+for m in 0 1 2; do
+  for c in 0 1; do
+    "$HIPCC" "${FLAGS[@]}" -DTA_FILL_MODE=$m -DTA_FILL_CIGAR=$c -c "$CS/ta_kernels.hip" -o "$B/ta_fill_$m$c.o" & pids+=($!)
+  done
+done
+"$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$CS/ta_kernels.hip" -o "$B/ta_misc.o" & pids+=($!)
+"$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip" -o "$B/ta_api.o" & pids+=($!)
+"$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp" -o "$B/shim.o" & pids+=($!)
+for p in "${pids[@]}"; do wait "$p"; done
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_api.o" "$B/shim.o" -o "$OUT"
 make -s -C "$ROOT/oracle" >/dev/null
 echo "built $OUT"
