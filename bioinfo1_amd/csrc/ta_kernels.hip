@@ -459,19 +459,28 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
 
 #ifdef TA_TU_MISC
 // ---------------------------------------------------------------------------
-// Traceback: one wave per pair, the walk itself is wave-uniform (SALU); the
-// wave's lanes only fetch 64-step x 4-lane tiles of the pointer matrix
-// (64 rows x ~64 columns) with one dwordx4 load each, and the walk reads codes
-// out of the tile with v_readlane.  The CIGAR is written right to left.
+// Traceback.  One wave per pair; the walk state (i, j) is wave-uniform and
+// lives in SGPRs.  The wave keeps a tile of the pointer matrix in 4 VGPRs:
+// wave-lane k holds the dwords of stripes L0..L0+3 at step tt0+k (64 steps x
+// 64 rows).  Each iteration resolves a whole run of one op instead of one
+// cell (SURVEY §7 "traceback latency"):
+//   D (vertical)   -- the rows above in the same dword: counted on the SALU
+//                     (xor with the D pattern, count trailing zero fields);
+//   I (horizontal) -- every wave-lane extracts row r of its step; the run is
+//                     the streak of I codes in the ballot going down from
+//                     the current step;
+//   M (diagonal)   -- every wave-lane extracts the diagonal cell of its step
+//                     (row r - (t - step)); same ballot streak.
+// Runs are clipped to the current stripe and tile; the next iteration picks
+// the walk up from there.  The CIGAR is written right to left into the slot.
 struct RleWriter {
     char* slot;
     uint64_t pos;
     uint32_t op, cnt;
     uint64_t total;
-    int lane;
     __device__ void put(char c) {
         --pos;
-        if (lane == 0) slot[pos] = c;
+        slot[pos] = c;  // every lane stores the same byte to the same address
     }
     __device__ void flush() {
         if (!cnt) return;
@@ -495,25 +504,25 @@ struct RleWriter {
     }
 };
 
+// length of the streak of set bits in b going down from bit `from` (>= 1 when bit `from` is set)
+__device__ __forceinline__ uint32_t streak_down(uint64_t b, uint32_t from) {
+    const uint64_t y = ~(b << (63u - from));  // bit `from` -> 63; shifted-in zeros stop the streak
+    return y ? (uint32_t)__clzll((long long)y) : 64u;
+}
+
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t widx = wave_id();
-    if (widx >= a.count) return;
-    const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
-    const uint32_t n = a.qlen[p], m = a.tlen[p];
-    const uint32_t gi = a.goal_i[p], gj = a.goal_j[p];
-    const uint64_t cap = cigar_slot_bytes(n, m);
-    RleWriter w{a.slots + a.slot_off[p], cap, 0u, 0u, 0ull, lane};
+__device__ void traceback_pair(const uint32_t* P, uint32_t n, uint32_t m, uint32_t gi, uint32_t gj, char* slot,
+                               uint64_t cap, int lane, uint64_t* start_in_slot, uint32_t* len) {
+    RleWriter w{slot, cap, 0u, 0u, 0ull};
     if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
         if (gi == n) w.push('I', m - gj);
         else if (gj == m) w.push('D', n - gi);
     }
-    const uint32_t* P = a.ptrs + a.ptr_off[p];
     const uint32_t Tmax = pass_steps(m);
     uint32_t i = gi, j = gj;
-    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tq = 0;
-    uint4 tile = make_uint4(0, 0, 0, 0);
+    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tL0 = 0;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    const int lane2 = 2 * lane;
     while (true) {
         if (MODE == kLocal) {
             if (i == 0 || j == 0) break;  // row/col 0 cost 0 ends the walk (:202)
@@ -532,30 +541,46 @@ __global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
         const uint32_t within = row % kPassRows;
         const uint32_t ln = within / kRows, r = within % kRows;
         const uint32_t t = (j - 1) + ln;
-        if (!(pass == tP && t >= tt0 && t < tt0 + 64u && (ln >> 2) == tq)) {
+        if (!(pass == tP && t >= tt0 && t < tt0 + 64u && ln >= tL0 && ln < tL0 + 4u)) {
             tP = pass;
-            tq = ln >> 2;
+            tL0 = ln >= 3u ? ln - 3u : 0u;
             tt0 = t >= 63u ? t - 63u : 0u;
             const uint32_t ts = tt0 + (uint32_t)lane;
-            tile = make_uint4(0, 0, 0, 0);
-            if (ts < Tmax)
-                tile = *reinterpret_cast<const uint4*>(P + ((uint64_t)pass * Tmax + ts) * kWave + tq * 4u);
+            c0 = c1 = c2 = c3 = 0;
+            if (ts < Tmax) {
+                const uint32_t* q = P + ((uint64_t)pass * Tmax + ts) * kWave + tL0;
+                c0 = q[0];
+                c1 = q[1];
+                c2 = q[2];
+                c3 = q[3];
+            }
         }
-        const uint32_t sel = ln & 3u;
-        const uint32_t comp = sel == 0 ? tile.x : sel == 1 ? tile.y : sel == 2 ? tile.z : tile.w;
-        const uint32_t dw = (uint32_t)rdlane((int)comp, t - tt0);
-        const uint32_t code = (dw >> (2u * (kRows - 1 - r))) & 3u;
+        const uint32_t sel = ln - tL0;
+        const uint32_t comp = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
+        const uint32_t kk = t - tt0;
+        const uint32_t dw = (uint32_t)rdlane((int)comp, kk);
+        const uint32_t fld = 30u - 2u * r;  // bit offset of row r's 2-bit code
+        const uint32_t code = (dw >> fld) & 3u;
         if (code == kCodeStop) break;  // local: cost == 0 (:202)
-        if (code == kCodeM) {
-            w.push('M', 1);
-            --i;
-            --j;
+        uint32_t run;
+        if (code == kCodeD) {
+            const uint32_t x = (dw ^ 0xAAAAAAAAu) >> fld;  // D fields of rows r, r-1, .. become 00
+            run = x ? ((uint32_t)__ffs((int)x) - 1u) >> 1 : 16u;
+            run = min(run, r + 1u);
+            w.push('D', run);
+            i -= run;
         } else if (code == kCodeI) {
-            w.push('I', 1);
-            --j;
+            const uint32_t v = __builtin_amdgcn_ubfe(comp, fld, 2u);  // row r at every step of the tile
+            run = min(streak_down(ballot(v == kCodeI), kk), j);
+            w.push('I', run);
+            j -= run;
         } else {
-            w.push('D', 1);
-            --i;
+            // diagonal: step tt0+lane holds row r - (kk - lane), bit offset fld + 2*(kk - lane)
+            const uint32_t v = __builtin_amdgcn_ubfe(comp, (uint32_t)((int)(fld + 2u * kk) - lane2), 2u);
+            run = min(min(streak_down(ballot(v == kCodeM), kk), r + 1u), j);
+            w.push('M', run);
+            i -= run;
+            j -= run;
         }
     }
     w.flush();
@@ -563,9 +588,24 @@ __global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
         w.put('\0');
         w.put('1');
     }
+    *start_in_slot = w.pos;
+    *len = (uint32_t)(cap - w.pos);
+}
+
+template <int MODE>
+__global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t widx = wave_id();
+    if (widx >= a.count) return;
+    const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
+    const uint32_t n = a.qlen[p], m = a.tlen[p];
+    uint64_t st;
+    uint32_t len;
+    traceback_pair<MODE>(a.ptrs + a.ptr_off[p], n, m, a.goal_i[p], a.goal_j[p], a.slots + a.slot_off[p],
+                         cigar_slot_bytes(n, m), lane, &st, &len);
     if (lane == 0) {
-        a.cigar_start[p] = a.slot_off[p] + w.pos;
-        a.cigar_len[p] = (uint32_t)(cap - w.pos);
+        a.cigar_start[p] = a.slot_off[p] + st;
+        a.cigar_len[p] = len;
     }
 }
 

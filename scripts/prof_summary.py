@@ -48,7 +48,7 @@ def main():
     if st:
         shutil.copy(st, os.path.join(prof, f"{rtag}_kernel_stats.csv"))
     pmc = {}
-    for part in ("prof_fetch", "prof_write", "prof_sq", "prof_busy"):
+    for part in ("prof_fetch", "prof_write", "prof_sq", "prof_busy", "prof_wait"):
         for k, cs in pmc_avgs(os.path.join(src, part)).items():
             pmc.setdefault(k, {}).update(cs)
     with open(os.path.join(prof, f"{rtag}_pmc.json"), "w") as fh:

@@ -25,4 +25,5 @@ step prof_fetch 600 --pmc FETCH_SIZE
 step prof_write 600 --pmc WRITE_SIZE
 step prof_sq 600 --pmc SQ_INSTS_VALU SQ_INSTS_SALU SQ_WAVES SQ_WAVE_CYCLES
 step prof_busy 600 --pmc SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_LDS SQ_INSTS_VMEM_WR
+step prof_wait 600 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_ANY
 echo "profile done" | tee -a "$OUT/profile.log"
