@@ -45,7 +45,10 @@ from bioinfo1_amd import synth  # noqa: E402
 from bioinfo1_amd.align import Aligner, DevicePlan  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, Chip-level parameters)
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # int32 lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz = 78.6 T
+# int32 VALU: a wave64 integer instruction occupies its SIMD for 4 cycles (measured:
+# SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU quad-cycles at ~100% busy), i.e. 16 lanes/clk/SIMD:
+# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T lane-ops/s
+VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 
 
 def parse():

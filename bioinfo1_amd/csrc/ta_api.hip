@@ -33,6 +33,7 @@ struct ta_plan {
     uint32_t n_pairs = 0;
     int type = 0, match = 0, mismatch = 0, gap = 0;
     bool want_cigar = false, wide = false;
+    bool fused = true;  // traceback inside the fill kernel (TA_FUSED_TRACEBACK=0 disables)
     std::vector<uint32_t> qlen, tlen, order;
     std::vector<uint64_t> slot_off;
     struct Chunk {
@@ -161,6 +162,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     pl->mismatch = mismatch;
     pl->gap = gap;
     pl->want_cigar = want_cigar != 0;
+    if (const char* e = std::getenv("TA_FUSED_TRACEBACK")) pl->fused = std::atoi(e) != 0;
     pl->qlen.assign(qlen, qlen + n_pairs);
     pl->tlen.assign(tlen, tlen + n_pairs);
     // Local mode keeps V = 32*score + row tag in int32; take the unscaled
@@ -264,9 +266,14 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         a.target_begin = io->target_begin;
         a.goal_i = pl->d_goal_i;
         a.goal_j = pl->d_goal_j;
+        a.fused = (pl->fused && pl->want_cigar) ? 1 : 0;
+        a.slots = io->cigar_slots;
+        a.slot_off = pl->d_slot_off;
+        a.cigar_start = io->cigar_start;
+        a.cigar_len = io->cigar_len;
         TA_HIP(pl->ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, a, s));
     }
-    if (trace && pl->want_cigar) {
+    if (trace && pl->want_cigar && !(fill && pl->fused)) {
         ta::TraceArgs t{};
         t.order = pl->d_order;
         t.begin = ch.begin;

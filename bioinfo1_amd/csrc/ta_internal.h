@@ -54,6 +54,12 @@ struct FillArgs {
     uint32_t* target_begin;
     uint32_t* goal_i;
     uint32_t* goal_j;
+    // fused traceback (fill kernel walks its own pair right after the fill)
+    int fused;
+    char* slots;
+    const uint64_t* slot_off;
+    uint64_t* cigar_start;
+    uint32_t* cigar_len;
 };
 
 struct TraceArgs {

@@ -91,7 +91,163 @@ __device__ __forceinline__ int load_bchunk(const int32_t* B, uint32_t m, uint32_
     return j <= m ? B[j] : 0;
 }
 
+// ---------------------------------------------------------------------------
+// Traceback.  One wave per pair; the walk state (i, j) is wave-uniform and
+// lives in SGPRs.  The wave keeps a tile of the pointer matrix in 4 VGPRs:
+// wave-lane k holds the dwords of stripes L0..L0+3 at step tt0+k (64 steps x
+// 64 rows).  Each iteration resolves a whole run of one op instead of one
+// cell (SURVEY §7 "traceback latency"):
+//   D (vertical)   -- the rows above in the same dword: counted on the SALU
+//                     (xor with the D pattern, count trailing zero fields);
+//   I (horizontal) -- every wave-lane extracts row r of its step; the run is
+//                     the streak of I codes in the ballot going down from
+//                     the current step;
+//   M (diagonal)   -- every wave-lane extracts the diagonal cell of its step
+//                     (row r - (t - step)); same ballot streak.
+// Runs are clipped to the current stripe and tile; the next iteration picks
+// the walk up from there.  The CIGAR is written right to left into the slot.
+struct RleWriter {
+    char* end;       // one past the slot's last byte; bytes go to end[-1], end[-2], ...
+    uint32_t used;   // bytes written so far
+    uint32_t op, cnt;
+    uint64_t total;
+    __device__ __forceinline__ void put(char c) {
+        ++used;
+        *(end - used) = c;  // every lane stores the same byte to the same address
+    }
+    __device__ __forceinline__ void flush() {
+        if (!cnt) return;
+        put((char)op);  // to_string(count) + op, written backwards
+        uint32_t c = cnt;
+        if (c < 10u) {
+            put((char)('0' + c));
+            return;
+        }
+        do {
+            const uint32_t q = c / 10u;
+            put((char)('0' + (c - 10u * q)));
+            c = q;
+        } while (c);
+    }
+    __device__ __forceinline__ void push(uint32_t o, uint32_t k) {
+        total += k;
+        if (o == op) {
+            cnt += k;
+        } else {
+            flush();
+            op = o;
+            cnt = k;
+        }
+    }
+};
+
+// length of the streak of set bits in b going down from bit `from` (>= 1 when bit `from` is set)
+__device__ __forceinline__ uint32_t streak_down(uint64_t b, uint32_t from) {
+    const uint64_t y = ~(b << (63u - from));  // bit `from` -> 63; shifted-in zeros stop the streak
+    return y ? (uint32_t)__clzll((long long)y) : 64u;
+}
+
+template <int MODE>
+__device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, uint32_t m, uint32_t gi, uint32_t gj,
+                                               char* slot, uint64_t cap, int lane, uint64_t* start_in_slot,
+                                               uint32_t* len) {
+    RleWriter w{slot + cap, 0u, 0u, 0u, 0ull};
+    if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
+        if (gi == n) {
+            if (m - gj) w.push('I', m - gj);
+        } else if (gj == m && n - gi) {
+            w.push('D', n - gi);
+        }
+    }
+    const uint32_t Tmax = pass_steps(m);
+    uint32_t i = gi, j = gj;
+    // tile = steps [tt0, tt0+64) x stripes [tL0, tL0+4) of pass tP.  The walk
+    // never moves to a larger step or stripe within a pass, so only the lower
+    // bounds (and the pass) need checking.
+    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tL0 = 0;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    const int lane2 = 2 * lane;
+    while (true) {
+        if (MODE == kLocal) {
+            if ((i == 0) | (j == 0)) break;  // row/col 0 cost 0 ends the walk (:202)
+        } else {
+            if (i == 0) {  // row 0: INSERT parents (:89-92)
+                if (j) w.push('I', j);
+                break;
+            }
+            if (j == 0) {  // column 0: DELETE parents (:83-86)
+                w.push('D', i);
+                break;
+            }
+        }
+        const uint32_t row = i - 1;
+        const uint32_t pass = row >> 10;  // kPassRows = 1024
+        const uint32_t ln = (row >> 4) & 63u, r = row & 15u;
+        const uint32_t t = (j - 1) + ln;
+        if (((int)((t - tt0) | (ln - tL0)) < 0) | (pass != tP)) {
+            tP = pass;
+            tL0 = ln >= 3u ? ln - 3u : 0u;
+            tt0 = t >= 63u ? t - 63u : 0u;
+            const uint32_t ts = tt0 + (uint32_t)lane;
+            c0 = c1 = c2 = c3 = 0;
+            if (ts < Tmax) {
+                const uint32_t* q = P + ((uint64_t)pass * Tmax + ts) * kWave + tL0;
+                c0 = q[0];
+                c1 = q[1];
+                c2 = q[2];
+                c3 = q[3];
+            }
+        }
+        const uint32_t sel = ln - tL0;
+        const uint32_t comp = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
+        const uint32_t kk = t - tt0;
+        const uint32_t dw = (uint32_t)rdlane((int)comp, kk);
+        const uint32_t fld = 30u - 2u * r;  // bit offset of row r's 2-bit code
+        const uint32_t code = (dw >> fld) & 3u;
+        if (code == kCodeStop) break;  // local: cost == 0 (:202)
+        uint32_t run;
+        if (code == kCodeD) {
+            const uint32_t x = (dw ^ 0xAAAAAAAAu) >> fld;  // D fields of rows r, r-1, .. become 00
+            run = x ? ((uint32_t)__ffs((int)x) - 1u) >> 1 : 16u;
+            run = min(run, r + 1u);
+            w.push('D', run);
+            i -= run;
+        } else if (code == kCodeI) {
+            const uint32_t v = __builtin_amdgcn_ubfe(comp, fld, 2u);  // row r at every step of the tile
+            run = min(streak_down(ballot(v == kCodeI), kk), j);
+            w.push('I', run);
+            j -= run;
+        } else {
+            // diagonal: step tt0+lane holds row r - (kk - lane), bit offset fld + 2*(kk - lane)
+            const uint32_t v = __builtin_amdgcn_ubfe(comp, (uint32_t)((int)(fld + 2u * kk) - lane2), 2u);
+            run = min(min(streak_down(ballot(v == kCodeM), kk), r + 1u), j);
+            w.push('M', run);
+            i -= run;
+            j -= run;
+        }
+    }
+    w.flush();
+    if (w.total == 0) {  // RLE of an empty string: "1" + '\0' (:145-160)
+        w.put('\0');
+        w.put('1');
+    }
+    *start_in_slot = cap - w.used;
+    *len = w.used;
+}
+
 #ifdef TA_FILL_MODE
+template <int MODE>
+__device__ __forceinline__ void fused_traceback(const FillArgs& a, uint32_t p, const uint32_t* ptrs, uint32_t n,
+                                                uint32_t m, uint32_t gi, uint32_t gj, int lane) {
+    uint64_t st;
+    uint32_t len;
+    traceback_pair<MODE>(ptrs, n, m, gi, gj, a.slots + a.slot_off[p], cigar_slot_bytes(n, m), lane, &st, &len);
+    if (lane == 0) {
+        a.cigar_start[p] = a.slot_off[p] + st;
+        a.cigar_len[p] = len;
+    }
+}
+
 // Degenerate pairs (an empty query or target): closed forms of what the
 // reference computes when one of its loops is empty.
 template <int MODE>
@@ -418,6 +574,11 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
     const uint32_t n = a.qlen[p], m = a.tlen[p];
     if (n == 0 || m == 0) {
         if (lane == 0) degenerate<MODE>(a, p, n, m);
+        if (CIGAR && a.fused) {
+            // no cells: the walk is the closed-form boundary run (global/semi) or "1\0"
+            const uint32_t gi = (MODE == kGlobal) ? n : 0, gj = (MODE == kGlobal || n == 0) ? m : 0;
+            fused_traceback<MODE>(a, p, nullptr, n, m, MODE == kLocal ? 0 : gi, MODE == kLocal ? 0 : gj, lane);
+        }
         return;
     }
     const uint8_t* Q = a.qbytes + a.qoff[p];
@@ -447,6 +608,13 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
         // the next pass reads this pass's bottom row (written by this wave)
         if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
     }
+    if (CIGAR && a.fused) {
+        // this wave's pointer stores -> its own loads in the walk
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        fused_traceback<MODE>(a, p, ptrs, n, m, (MODE == kGlobal) ? n : best_i, (MODE == kGlobal) ? m : best_j,
+                              lane);
+    }
     if (lane == 0) {
         a.score[p] = (MODE == kGlobal) ? corner : best_h;
         a.target_begin[p] = (MODE == kLocal) ? best_j + 1 : 0;  // :117-121 / :197-199 / :283-285
@@ -458,140 +626,6 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
 #endif  // TA_FILL_MODE
 
 #ifdef TA_TU_MISC
-// ---------------------------------------------------------------------------
-// Traceback.  One wave per pair; the walk state (i, j) is wave-uniform and
-// lives in SGPRs.  The wave keeps a tile of the pointer matrix in 4 VGPRs:
-// wave-lane k holds the dwords of stripes L0..L0+3 at step tt0+k (64 steps x
-// 64 rows).  Each iteration resolves a whole run of one op instead of one
-// cell (SURVEY §7 "traceback latency"):
-//   D (vertical)   -- the rows above in the same dword: counted on the SALU
-//                     (xor with the D pattern, count trailing zero fields);
-//   I (horizontal) -- every wave-lane extracts row r of its step; the run is
-//                     the streak of I codes in the ballot going down from
-//                     the current step;
-//   M (diagonal)   -- every wave-lane extracts the diagonal cell of its step
-//                     (row r - (t - step)); same ballot streak.
-// Runs are clipped to the current stripe and tile; the next iteration picks
-// the walk up from there.  The CIGAR is written right to left into the slot.
-struct RleWriter {
-    char* slot;
-    uint64_t pos;
-    uint32_t op, cnt;
-    uint64_t total;
-    __device__ void put(char c) {
-        --pos;
-        slot[pos] = c;  // every lane stores the same byte to the same address
-    }
-    __device__ void flush() {
-        if (!cnt) return;
-        put((char)op);  // to_string(count) + op, written backwards
-        uint32_t c = cnt;
-        do {
-            put((char)('0' + c % 10u));
-            c /= 10u;
-        } while (c);
-    }
-    __device__ void push(uint32_t o, uint32_t k) {
-        if (!k) return;
-        total += k;
-        if (o == op) {
-            cnt += k;
-        } else {
-            flush();
-            op = o;
-            cnt = k;
-        }
-    }
-};
-
-// length of the streak of set bits in b going down from bit `from` (>= 1 when bit `from` is set)
-__device__ __forceinline__ uint32_t streak_down(uint64_t b, uint32_t from) {
-    const uint64_t y = ~(b << (63u - from));  // bit `from` -> 63; shifted-in zeros stop the streak
-    return y ? (uint32_t)__clzll((long long)y) : 64u;
-}
-
-template <int MODE>
-__device__ void traceback_pair(const uint32_t* P, uint32_t n, uint32_t m, uint32_t gi, uint32_t gj, char* slot,
-                               uint64_t cap, int lane, uint64_t* start_in_slot, uint32_t* len) {
-    RleWriter w{slot, cap, 0u, 0u, 0ull};
-    if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
-        if (gi == n) w.push('I', m - gj);
-        else if (gj == m) w.push('D', n - gi);
-    }
-    const uint32_t Tmax = pass_steps(m);
-    uint32_t i = gi, j = gj;
-    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tL0 = 0;
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    const int lane2 = 2 * lane;
-    while (true) {
-        if (MODE == kLocal) {
-            if (i == 0 || j == 0) break;  // row/col 0 cost 0 ends the walk (:202)
-        } else {
-            if (i == 0) {  // row 0: INSERT parents (:89-92)
-                w.push('I', j);
-                break;
-            }
-            if (j == 0) {  // column 0: DELETE parents (:83-86)
-                w.push('D', i);
-                break;
-            }
-        }
-        const uint32_t row = i - 1;
-        const uint32_t pass = row / kPassRows;
-        const uint32_t within = row % kPassRows;
-        const uint32_t ln = within / kRows, r = within % kRows;
-        const uint32_t t = (j - 1) + ln;
-        if (!(pass == tP && t >= tt0 && t < tt0 + 64u && ln >= tL0 && ln < tL0 + 4u)) {
-            tP = pass;
-            tL0 = ln >= 3u ? ln - 3u : 0u;
-            tt0 = t >= 63u ? t - 63u : 0u;
-            const uint32_t ts = tt0 + (uint32_t)lane;
-            c0 = c1 = c2 = c3 = 0;
-            if (ts < Tmax) {
-                const uint32_t* q = P + ((uint64_t)pass * Tmax + ts) * kWave + tL0;
-                c0 = q[0];
-                c1 = q[1];
-                c2 = q[2];
-                c3 = q[3];
-            }
-        }
-        const uint32_t sel = ln - tL0;
-        const uint32_t comp = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
-        const uint32_t kk = t - tt0;
-        const uint32_t dw = (uint32_t)rdlane((int)comp, kk);
-        const uint32_t fld = 30u - 2u * r;  // bit offset of row r's 2-bit code
-        const uint32_t code = (dw >> fld) & 3u;
-        if (code == kCodeStop) break;  // local: cost == 0 (:202)
-        uint32_t run;
-        if (code == kCodeD) {
-            const uint32_t x = (dw ^ 0xAAAAAAAAu) >> fld;  // D fields of rows r, r-1, .. become 00
-            run = x ? ((uint32_t)__ffs((int)x) - 1u) >> 1 : 16u;
-            run = min(run, r + 1u);
-            w.push('D', run);
-            i -= run;
-        } else if (code == kCodeI) {
-            const uint32_t v = __builtin_amdgcn_ubfe(comp, fld, 2u);  // row r at every step of the tile
-            run = min(streak_down(ballot(v == kCodeI), kk), j);
-            w.push('I', run);
-            j -= run;
-        } else {
-            // diagonal: step tt0+lane holds row r - (kk - lane), bit offset fld + 2*(kk - lane)
-            const uint32_t v = __builtin_amdgcn_ubfe(comp, (uint32_t)((int)(fld + 2u * kk) - lane2), 2u);
-            run = min(min(streak_down(ballot(v == kCodeM), kk), r + 1u), j);
-            w.push('M', run);
-            i -= run;
-            j -= run;
-        }
-    }
-    w.flush();
-    if (w.total == 0) {  // RLE of an empty string: "1" + '\0' (:145-160)
-        w.put('\0');
-        w.put('1');
-    }
-    *start_in_slot = w.pos;
-    *len = (uint32_t)(cap - w.pos);
-}
-
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
     const int lane = threadIdx.x & 63;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Static instruction census of the loops in a compiled kernel.
 
-  python scripts/isa_census.py <kernel-substring> [asm.s]
+  TA_CENSUS_FLAGS="-DTA_TU_MISC" python scripts/isa_census.py <kernel-substring> [asm.s]
 
 Builds bioinfo1_amd/csrc/ta_kernels.hip with -save-temps (unless an .s is
 given), finds the kernel whose symbol contains the substring, and for each
@@ -22,7 +22,8 @@ def asm_text(path=None):
         return open(path).read()
     out = "/tmp/ta_census"
     os.makedirs(out, exist_ok=True)
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "-c",
+    extra = os.environ.get("TA_CENSUS_FLAGS", "-DTA_FILL_MODE=1 -DTA_FILL_CIGAR=1").split()
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", *extra, "-c",
                            os.path.join(ROOT, "bioinfo1_amd/csrc/ta_kernels.hip"), "-o", f"{out}/k.o", "-save-temps"],
                           cwd=out, stderr=subprocess.DEVNULL)
     return open(f"{out}/ta_kernels-hip-amdgcn-amd-amdhsa-gfx950.s").read()
