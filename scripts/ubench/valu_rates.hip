@@ -1,0 +1,72 @@
+// scripts/ubench/valu_rates.hip -- cycles per wave-instruction for the VALU
+// ops the DP kernels use (MI355X).  Each kernel runs 8 independent chains of
+// one op per wave, 8 waves per SIMD, and reports the chip-wide rate.
+// Build + run on the GPU box: hipcc -O3 --offload-arch=gfx950 valu_rates.hip -o vr && ./vr
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+
+#define CHAINS 8
+#define ITERS 4096
+#define OPK(name, asmop)                                                                  \
+    __global__ void name(uint32_t* out, uint32_t seed) {                                  \
+        uint32_t v[CHAINS];                                                               \
+        for (int c = 0; c < CHAINS; ++c) v[c] = seed + threadIdx.x * 7u + c;             \
+        uint32_t k = seed | 0x00010001u;                                                  \
+        for (int i = 0; i < ITERS; ++i) {                                                 \
+            _Pragma("unroll") for (int c = 0; c < CHAINS; ++c) asm volatile(asmop : "+v"(v[c]) : "v"(k)); \
+        }                                                                                 \
+        uint32_t s = 0;                                                                   \
+        for (int c = 0; c < CHAINS; ++c) s ^= v[c];                                       \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = s;                                   \
+    }
+OPK(k_add_u32, "v_add_u32 %0, %0, %1")
+OPK(k_max_i32, "v_max_i32 %0, %0, %1")
+OPK(k_max3_i32, "v_max3_i32 %0, %0, %1, %0")
+OPK(k_pk_add_u16, "v_pk_add_u16 %0, %0, %1")
+OPK(k_pk_max_i16, "v_pk_max_i16 %0, %0, %1")
+OPK(k_pk_min_u16, "v_pk_min_u16 %0, %0, %1")
+OPK(k_pk_mad_i16, "v_pk_mad_i16 %0, %0, %1, %0")
+OPK(k_perm, "v_perm_b32 %0, %0, %1, %0")
+OPK(k_xor, "v_xor_b32 %0, %0, %1")
+OPK(k_cndmask, "v_cndmask_b32 %0, %0, %1, vcc")
+OPK(k_addc, "v_addc_co_u32 %0, vcc, %0, %0, vcc")
+OPK(k_bfe, "v_bfe_u32 %0, %0, %1, 2")
+OPK(k_lshl_or, "v_lshl_or_b32 %0, %0, 1, %1")
+OPK(k_pk_fma_f32_probe, "v_pk_add_u16 %0, %0, %1 op_sel_hi:[1,1]")
+
+int main() {
+    int dev = 0;
+    hipDeviceProp_t p;
+    hipGetDeviceProperties(&p, dev);
+    const int cus = p.multiProcessorCount;
+    const int waves_per_simd = 8, block = 256;
+    const int blocks = cus * 4 * waves_per_simd * 64 / block;
+    uint32_t* out;
+    hipMalloc(&out, (size_t)blocks * block * 4);
+    struct K { const char* n; void (*f)(uint32_t*, uint32_t); } ks[] = {
+        {"v_add_u32", k_add_u32}, {"v_max_i32", k_max_i32}, {"v_max3_i32", k_max3_i32},
+        {"v_pk_add_u16", k_pk_add_u16}, {"v_pk_max_i16", k_pk_max_i16}, {"v_pk_min_u16", k_pk_min_u16},
+        {"v_pk_mad_i16", k_pk_mad_i16}, {"v_perm_b32", k_perm}, {"v_xor_b32", k_xor},
+        {"v_cndmask_b32", k_cndmask}, {"v_addc_co_u32", k_addc}, {"v_bfe_u32", k_bfe},
+        {"v_lshl_or_b32", k_lshl_or}, {"v_pk_add_u16(opsel)", k_pk_fma_f32_probe}};
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    printf("CUs %d, clock %d kHz, %d waves/SIMD\n", cus, p.clockRate, waves_per_simd);
+    for (auto& k : ks) {
+        hipLaunchKernelGGL(k.f, dim3(blocks), dim3(block), 0, 0, out, 1u);
+        hipDeviceSynchronize();
+        hipEventRecord(a);
+        for (int r = 0; r < 5; ++r) hipLaunchKernelGGL(k.f, dim3(blocks), dim3(block), 0, 0, out, (uint32_t)r);
+        hipEventRecord(b);
+        hipEventSynchronize(b);
+        float ms;
+        hipEventElapsedTime(&ms, a, b);
+        const double winstr = 5.0 * blocks * (block / 64) * (double)ITERS * CHAINS;
+        const double per_simd_per_s = winstr / (ms * 1e-3) / (cus * 4);
+        printf("%-22s %8.3f ms  %.3f Gwave-instr/s/SIMD  => %.2f cycles/wave-instr at 2.4 GHz\n", k.n, ms,
+               per_simd_per_s / 1e9, 2.4e9 / per_simd_per_s);
+    }
+    return 0;
+}
