@@ -67,6 +67,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal only)")
     return ap.parse_args()
 
 
@@ -143,9 +144,11 @@ def main():
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+        dist.init_process_group(args.dist_backend)
+    # TA_BENCH_ONE_GPU=1: every rank on device 0 (multi-rank rehearsal on a 1-GPU box, gloo)
+    dev_index = 0 if os.environ.get("TA_BENCH_ONE_GPU") == "1" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     mode = MODES[args.mode]
     sc = tuple(int(x) for x in args.scoring.split(","))
     cigar = not args.no_cigar
@@ -155,11 +158,12 @@ def main():
     gen = synth.related_batch if args.related else synth.uniform_batch
     batch = gen(P, args.qlen, args.tlen, 0x5EED, first_pair=rank * P)
 
-    al = Aligner(local_rank)
+    al = Aligner(dev_index)
     plan = DevicePlan(al, batch, mode, *sc, cigar)
     stream = torch.cuda.current_stream(dev)
-    rec = torch.zeros((3, P), dtype=torch.int32, device=dev)
-    gathered = torch.zeros((world, 3, P), dtype=torch.int32, device=dev) if world > 1 else None
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo: host tensors
+    rec = torch.zeros((3, P), dtype=torch.int32, device=coll_dev)
+    gathered = torch.zeros((world, 3, P), dtype=torch.int32, device=coll_dev) if world > 1 else None
 
     def step():
         plan.run()
@@ -190,7 +194,7 @@ def main():
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
     if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        e = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         elapsed = float(e.item())
     ms = elapsed / max(args.steps, 1) * 1e3

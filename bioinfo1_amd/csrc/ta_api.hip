@@ -34,16 +34,20 @@ struct ta_plan {
     int type = 0, match = 0, mismatch = 0, gap = 0;
     bool want_cigar = false, wide = false;
     bool fused = true;  // traceback inside the fill kernel (TA_FUSED_TRACEBACK=0 disables)
-    std::vector<uint32_t> qlen, tlen, order;
+    bool dual = true;   // packed two-pair int16 fill where it fits (TA_DUAL=0 disables)
+    std::vector<uint32_t> qlen, tlen, order, singles, duals;
     std::vector<uint64_t> slot_off;
     struct Chunk {
-        uint32_t begin, count;
+        uint32_t begin, count;    // all pairs (traceback order)
+        uint32_t sbegin, scount;  // int32 fill: pairs
+        uint32_t dbegin, dcount;  // dual fill: pair couples
         uint64_t ptr_dwords, bnd_words;
     };
+    uint32_t n_dual_pairs = 0;
     std::vector<Chunk> chunks;
     uint64_t slots_bytes = 0, ws_ptr_dwords = 0, ws_bnd_words = 0;
     // device
-    uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr;
+    uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr, *d_singles = nullptr, *d_duals = nullptr;
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
     uint32_t *d_goal_i = nullptr, *d_goal_j = nullptr;
     uint32_t* d_ptrs = nullptr;
@@ -141,7 +145,7 @@ void ta_context_destroy(ta_context* ctx) {
 void ta_plan_destroy(ta_plan* pl) {
     if (!pl) return;
     (void)hipSetDevice(pl->ctx->device);
-    for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_ptr_off,
+    for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_ptr_off,
                     (void*)pl->d_bnd_off, (void*)pl->d_slot_off, (void*)pl->d_goal_i, (void*)pl->d_goal_j,
                     (void*)pl->d_ptrs, (void*)pl->d_bnd})
         if (p) (void)hipFree(p);
@@ -172,11 +176,15 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     const uint64_t mag = std::max<uint64_t>({1ull, (uint64_t)std::llabs(match), (uint64_t)std::llabs(mismatch),
                                              (uint64_t)std::llabs(gap)});
     pl->wide = (type == TA_LOCAL) && (maxlen * mag >= (1ull << 25));
-    // Longest pairs first (fewer stragglers), stable for equal cell counts.
+    if (const char* e = std::getenv("TA_DUAL")) pl->dual = std::atoi(e) != 0;
+    // Longest pairs first (fewer stragglers); equal shapes adjacent so they
+    // can be coupled for the two-pair kernel.
     pl->order.resize(n_pairs);
     std::iota(pl->order.begin(), pl->order.end(), 0u);
     std::stable_sort(pl->order.begin(), pl->order.end(), [&](uint32_t a, uint32_t b) {
-        return (uint64_t)pl->qlen[a] * pl->tlen[a] > (uint64_t)pl->qlen[b] * pl->tlen[b];
+        const uint64_t ca = (uint64_t)pl->qlen[a] * pl->tlen[a], cb = (uint64_t)pl->qlen[b] * pl->tlen[b];
+        if (ca != cb) return ca > cb;
+        return pl->qlen[a] != pl->qlen[b] ? pl->qlen[a] > pl->qlen[b] : pl->tlen[a] > pl->tlen[b];
     });
     if (budget == 0) budget = default_budget();
     const uint64_t budget_dw = std::max<uint64_t>(budget / 4, 1);
@@ -188,20 +196,40 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
         so += ta::cigar_slot_bytes(pl->qlen[p], pl->tlen[p]);
     }
     pl->slots_bytes = so;
-    ta_plan::Chunk cur{0, 0, 0, 0};
-    for (uint32_t k = 0; k < n_pairs; ++k) {
+    ta_plan::Chunk cur{0, 0, 0, 0, 0, 0, 0, 0};
+    auto open_chunk = [&](uint32_t k) {
+        cur = ta_plan::Chunk{k, 0, (uint32_t)pl->singles.size(), 0, (uint32_t)(pl->duals.size() / 2), 0, 0, 0};
+    };
+    open_chunk(0);
+    for (uint32_t k = 0; k < n_pairs;) {
         const uint32_t p = pl->order[k];
-        const uint64_t pd = pl->want_cigar ? ta::ptr_dwords(pl->qlen[p], pl->tlen[p]) : 0;
-        const uint64_t bw = ta::bnd_words(pl->qlen[p], pl->tlen[p]);
+        const uint32_t n = pl->qlen[p], m = pl->tlen[p];
+        const bool couple = pl->dual && k + 1 < n_pairs && pl->qlen[pl->order[k + 1]] == n &&
+                            pl->tlen[pl->order[k + 1]] == m && ta::fits_int16(type, n, m, match, mismatch, gap);
+        const uint32_t units = couple ? 2 : 1;
+        const uint64_t pd = pl->want_cigar ? units * ta::ptr_dwords(n, m) : 0;
         if (cur.count && cur.ptr_dwords + pd > budget_dw) {
             pl->chunks.push_back(cur);
-            cur = ta_plan::Chunk{k, 0, 0, 0};
+            open_chunk(k);
         }
-        ptr_off[p] = cur.ptr_dwords;
-        bnd_off[p] = cur.bnd_words;
-        cur.ptr_dwords += pd;
-        cur.bnd_words += bw;
-        ++cur.count;
+        for (uint32_t u = 0; u < units; ++u) {
+            const uint32_t q = pl->order[k + u];
+            ptr_off[q] = cur.ptr_dwords;
+            bnd_off[q] = cur.bnd_words;
+            cur.ptr_dwords += pl->want_cigar ? ta::ptr_dwords(n, m) : 0;
+            cur.bnd_words += ta::bnd_words(n, m);
+        }
+        if (couple) {
+            pl->duals.push_back(p);
+            pl->duals.push_back(pl->order[k + 1]);
+            ++cur.dcount;
+            pl->n_dual_pairs += 2;
+        } else {
+            pl->singles.push_back(p);
+            ++cur.scount;
+        }
+        cur.count += units;
+        k += units;
     }
     if (cur.count) pl->chunks.push_back(cur);
     for (auto& c : pl->chunks) {
@@ -215,6 +243,8 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     up(upload(ctx, &pl->d_qlen, pl->qlen));
     up(upload(ctx, &pl->d_tlen, pl->tlen));
     up(upload(ctx, &pl->d_order, pl->order));
+    up(upload(ctx, &pl->d_singles, pl->singles));
+    up(upload(ctx, &pl->d_duals, pl->duals));
     up(upload(ctx, &pl->d_ptr_off, ptr_off));
     up(upload(ctx, &pl->d_bnd_off, bnd_off));
     up(upload(ctx, &pl->d_slot_off, pl->slot_off));
@@ -241,6 +271,7 @@ uint64_t ta_plan_workspace_bytes(const ta_plan* pl) {
     return pl ? (pl->ws_ptr_dwords + pl->ws_bnd_words) * 4ull : 0;
 }
 uint32_t ta_plan_chunks(const ta_plan* pl) { return pl ? (uint32_t)pl->chunks.size() : 0; }
+uint32_t ta_plan_dual_pairs(const ta_plan* pl) { return pl ? pl->n_dual_pairs : 0; }
 
 static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill, bool trace) {
     const auto& ch = pl->chunks[c];
@@ -271,7 +302,19 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         a.slot_off = pl->d_slot_off;
         a.cigar_start = io->cigar_start;
         a.cigar_len = io->cigar_len;
-        TA_HIP(pl->ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, a, s));
+        if (ch.dcount) {
+            ta::FillArgs d = a;
+            d.order = pl->d_duals;
+            d.begin = ch.dbegin;
+            d.count = ch.dcount;
+            TA_HIP(pl->ctx, ta::launch_dual(pl->type, pl->want_cigar, d, s));
+        }
+        if (ch.scount) {
+            a.order = pl->d_singles;
+            a.begin = ch.sbegin;
+            a.count = ch.scount;
+            TA_HIP(pl->ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, a, s));
+        }
     }
     if (trace && pl->want_cigar && !(fill && pl->fused)) {
         ta::TraceArgs t{};

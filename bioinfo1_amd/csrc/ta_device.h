@@ -1,0 +1,258 @@
+// bioinfo1_amd/csrc/ta_device.h -- device helpers shared by the int32 kernels
+// (ta_kernels.hip) and the packed dual-pair kernels (ta_dual.hip): wave
+// primitives, target/boundary chunk loads, and the run-jumping traceback.
+#pragma once
+
+#include <climits>
+#include <type_traits>
+
+#include "ta_internal.h"
+
+namespace ta {
+namespace {
+
+
+__device__ __forceinline__ int wadd(int a, int b) { return (int)((uint32_t)a + (uint32_t)b); }
+__device__ __forceinline__ int wmul(uint32_t a, int b) { return (int)(a * (uint32_t)b); }
+
+// DPP wave_shr:1 -- lane l gets v of lane l-1, lane 0 gets `lane0`.
+// Must run with all 64 lanes enabled.
+__device__ __forceinline__ int wave_shr1(int lane0, int v) {
+    return __builtin_amdgcn_update_dpp(lane0, v, 0x138, 0xF, 0xF, false);
+}
+
+__device__ __forceinline__ int rdlane(int v, uint32_t l) { return __builtin_amdgcn_readlane(v, (int)l); }
+
+// Global wave index.  readfirstlane tells the compiler it is wave-uniform
+// (threadIdx.x >> 6 is not provably so), which keeps the pair's lengths, the
+// loop counters and all per-pair control flow in SGPRs / scalar branches.
+__device__ __forceinline__ uint32_t wave_id() {
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)(blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)));
+}
+
+__device__ __forceinline__ uint64_t ballot(bool c) { return __builtin_amdgcn_ballot_w64(c); }
+
+// acc*2 + (this lane's bit of `mask`) in one v_addc_co_u32 (the lane mask is
+// the carry-in).  hipcc does not form this from C++ (it emits a cndmask +
+// shift + or), so it is spelled out.
+__device__ __forceinline__ uint32_t shl1_add_lanebit(uint32_t acc, uint64_t mask) {
+    uint32_t r;
+    uint64_t carry_out;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(carry_out) : "v"(acc), "s"(mask));
+    return r;
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v = max(v, __shfl_xor(v, o, 64));
+    return v;
+}
+
+__device__ __forceinline__ int first_lane(bool c) {
+    const unsigned long long b = __ballot(c);
+    return b ? __ffsll((long long)b) - 1 : -1;
+}
+
+// 256 target characters per chunk, 4 per lane; out-of-range bytes are 0.
+__device__ __forceinline__ uint32_t load_tchunk(const uint8_t* T, uint32_t m, uint32_t k, int lane) {
+    const uint32_t base = k * 256u + 4u * (uint32_t)lane;
+    uint32_t w = 0;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const uint32_t idx = base + b;
+        const uint32_t c = idx < m ? (uint32_t)T[idx] : 0u;
+        w |= c << (8 * b);
+    }
+    return w;
+}
+
+// 64 boundary-row values per chunk: column 64k+lane+1.
+__device__ __forceinline__ int load_bchunk(const int32_t* B, uint32_t m, uint32_t k, int lane) {
+    const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+    return j <= m ? B[j] : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Traceback.  One wave per pair; the walk state (i, j) is wave-uniform and
+// lives in SGPRs.  The wave keeps a tile of the pointer matrix in 4 VGPRs:
+// wave-lane k holds the dwords of stripes L0..L0+3 at step tt0+k (64 steps x
+// 64 rows).  Each iteration resolves a whole run of one op instead of one
+// cell (SURVEY §7 "traceback latency"):
+//   D (vertical)   -- the rows above in the same dword: counted on the SALU
+//                     (xor with the D pattern, count trailing zero fields);
+//   I (horizontal) -- every wave-lane extracts row r of its step; the run is
+//                     the streak of I codes in the ballot going down from
+//                     the current step;
+//   M (diagonal)   -- every wave-lane extracts the diagonal cell of its step
+//                     (row r - (t - step)); same ballot streak.
+// Runs are clipped to the current stripe and tile; the next iteration picks
+// the walk up from there.  The CIGAR is written right to left into the slot.
+struct RleWriter {
+    char* end;       // one past the slot's last byte; bytes go to end[-1], end[-2], ...
+    uint32_t used;   // bytes written so far
+    uint32_t op, cnt;
+    uint64_t total;
+    __device__ __forceinline__ void put(char c) {
+        ++used;
+        *(end - used) = c;  // every lane stores the same byte to the same address
+    }
+    __device__ __forceinline__ void flush() {
+        if (!cnt) return;
+        put((char)op);  // to_string(count) + op, written backwards
+        uint32_t c = cnt;
+        if (c < 10u) {
+            put((char)('0' + c));
+            return;
+        }
+        do {
+            const uint32_t q = c / 10u;
+            put((char)('0' + (c - 10u * q)));
+            c = q;
+        } while (c);
+    }
+    __device__ __forceinline__ void push(uint32_t o, uint32_t k) {
+        total += k;
+        if (o == op) {
+            cnt += k;
+        } else {
+            flush();
+            op = o;
+            cnt = k;
+        }
+    }
+};
+
+// length of the streak of set bits in b going down from bit `from` (>= 1 when bit `from` is set)
+__device__ __forceinline__ uint32_t streak_down(uint64_t b, uint32_t from) {
+    const uint64_t y = ~(b << (63u - from));  // bit `from` -> 63; shifted-in zeros stop the streak
+    return y ? (uint32_t)__clzll((long long)y) : 64u;
+}
+
+template <int MODE>
+__device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, uint32_t m, uint32_t gi, uint32_t gj,
+                                               char* slot, uint64_t cap, int lane, uint64_t* start_in_slot,
+                                               uint32_t* len) {
+    RleWriter w{slot + cap, 0u, 0u, 0u, 0ull};
+    if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
+        if (gi == n) {
+            if (m - gj) w.push('I', m - gj);
+        } else if (gj == m && n - gi) {
+            w.push('D', n - gi);
+        }
+    }
+    const uint32_t Tmax = pass_steps(m);
+    uint32_t i = gi, j = gj;
+    // tile = steps [tt0, tt0+64) x stripes [tL0, tL0+4) of pass tP.  The walk
+    // never moves to a larger step or stripe within a pass, so only the lower
+    // bounds (and the pass) need checking.
+    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tL0 = 0;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    const int lane2 = 2 * lane;
+    while (true) {
+        if (MODE == kLocal) {
+            if ((i == 0) | (j == 0)) break;  // row/col 0 cost 0 ends the walk (:202)
+        } else {
+            if (i == 0) {  // row 0: INSERT parents (:89-92)
+                if (j) w.push('I', j);
+                break;
+            }
+            if (j == 0) {  // column 0: DELETE parents (:83-86)
+                w.push('D', i);
+                break;
+            }
+        }
+        const uint32_t row = i - 1;
+        const uint32_t pass = row >> 10;  // kPassRows = 1024
+        const uint32_t ln = (row >> 4) & 63u, r = row & 15u;
+        const uint32_t t = (j - 1) + ln;
+        if (((int)((t - tt0) | (ln - tL0)) < 0) | (pass != tP)) {
+            tP = pass;
+            tL0 = ln >= 3u ? ln - 3u : 0u;
+            tt0 = t >= 63u ? t - 63u : 0u;
+            const uint32_t ts = tt0 + (uint32_t)lane;
+            c0 = c1 = c2 = c3 = 0;
+            if (ts < Tmax) {
+                const uint32_t* q = P + ((uint64_t)pass * Tmax + ts) * kWave + tL0;
+                c0 = q[0];
+                c1 = q[1];
+                c2 = q[2];
+                c3 = q[3];
+            }
+        }
+        const uint32_t sel = ln - tL0;
+        const uint32_t comp = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
+        const uint32_t kk = t - tt0;
+        const uint32_t dw = (uint32_t)rdlane((int)comp, kk);
+        const uint32_t fld = 30u - 2u * r;  // bit offset of row r's 2-bit code
+        const uint32_t code = (dw >> fld) & 3u;
+        if (code == kCodeStop) break;  // local: cost == 0 (:202)
+        uint32_t run;
+        if (code == kCodeD) {
+            const uint32_t x = (dw ^ 0xAAAAAAAAu) >> fld;  // D fields of rows r, r-1, .. become 00
+            run = x ? ((uint32_t)__ffs((int)x) - 1u) >> 1 : 16u;
+            run = min(run, r + 1u);
+            w.push('D', run);
+            i -= run;
+        } else if (code == kCodeI) {
+            const uint32_t v = __builtin_amdgcn_ubfe(comp, fld, 2u);  // row r at every step of the tile
+            run = min(streak_down(ballot(v == kCodeI), kk), j);
+            w.push('I', run);
+            j -= run;
+        } else {
+            // diagonal: step tt0+lane holds row r - (kk - lane), bit offset fld + 2*(kk - lane)
+            const uint32_t v = __builtin_amdgcn_ubfe(comp, (uint32_t)((int)(fld + 2u * kk) - lane2), 2u);
+            run = min(min(streak_down(ballot(v == kCodeM), kk), r + 1u), j);
+            w.push('M', run);
+            i -= run;
+            j -= run;
+        }
+    }
+    w.flush();
+    if (w.total == 0) {  // RLE of an empty string: "1" + '\0' (:145-160)
+        w.put('\0');
+        w.put('1');
+    }
+    *start_in_slot = cap - w.used;
+    *len = w.used;
+}
+
+// Select v[idx] for a wave-uniform runtime idx without dynamic register
+// indexing (which the compiler would lower through LDS or scratch).
+template <int R>
+__device__ __forceinline__ int select_row(const int (&v)[R], uint32_t idx) {
+    int x = 0;
+#pragma unroll
+    for (int k = 0; k < R; ++k) x |= v[k] & -(int)(idx == (uint32_t)k);
+    return x;
+}
+
+// Compile-time loop: f(std::integral_constant<int, I>) for I in [B, E).
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
+
+template <int C>
+__device__ __forceinline__ int max3_imm(int a, int b) {
+    // max(a, b, C) with C an inline constant.  Kept opaque so that hipcc does
+    // not split it back into two v_max when a later compare reads the result
+    // (it rewrites h == C into max(a,b) <= C).
+    int r;
+    asm("v_max3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "i"(C));
+    return r;
+}
+
+// What one pass reports to the running goal.
+struct PassOut {
+    int h;           // local: best score of the pass; semi: best of column m
+    uint32_t i, j;   // its cell (1-based rows), i == 0 when no candidate
+    int row_h;       // semi, last pass: best of row n
+    uint32_t row_j;
+    int corner;      // global, last pass: H[n][m]
+};
+
+}  // namespace
+}  // namespace ta

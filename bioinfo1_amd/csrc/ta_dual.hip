@@ -1,0 +1,421 @@
+// bioinfo1_amd/csrc/ta_dual.hip -- the DP fill for TWO pairs per wave in
+// packed 16-bit lanes (gfx950 v_pk_* ops), for batches of equal-length pairs
+// whose scores fit int16.  Same results as fill_kernel (ta_kernels.hip) and
+// the same 2-bit pointer codes, so the traceback is shared.
+//
+// Each 32-bit register holds pair A in bits 15:0 and pair B in bits 31:16.
+// The stored value is not H itself but a biased S chosen so that the
+// diagonal candidate costs ONE v_pk_mad_i16 (e * (mi-ma) + S_diag, with
+// e = min(q ^ t, 1) per half) and the other two one v_pk_add each:
+//   global / semi:  S = H - ma*j
+//   local:          S = 16*H + (1 - 16*ma)*j - i
+//     (the -i term tags the row: within a step S - Zbase + 15 = 16H + 15 - r
+//      is the reference's row-major first-max key; the clamp H >= 0 becomes
+//      S >= (1-16ma)j - i, a per-lane-per-step base minus the row index)
+// A cell's inputs move exactly as in fill_kernel (lane skew, DPP wave_shr:1).
+// Compares for the pointer codes are per half (SDWA word selects); the lane
+// masks are canonicalised on the SALU and shifted into one dword per pair
+// per lane per step with v_addc, exactly like the int32 kernel.
+#include "ta_device.h"
+
+namespace ta {
+namespace {
+
+#ifdef TA_DUAL_MODE
+
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, a) + __builtin_bit_cast(s2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, a) - __builtin_bit_cast(s2, b));
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, a), __builtin_bit_cast(s2, b)));
+}
+// max over v[B..E) as a balanced tree
+template <int B, int E>
+__device__ __forceinline__ uint32_t tree_max(const uint32_t* v) {
+    if constexpr (E - B == 1) return v[B];
+    else return pk_max(tree_max<B, (B + E) / 2>(v), tree_max<(B + E) / 2, E>(v));
+}
+// hipcc does not form these two from vector C++ (it expands min(x,1) into
+// compares + selects), so they are spelled out.
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t pk_mad_i16(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm("v_pk_mad_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+// per-half signed compares -> wave lane masks (one SDWA compare each)
+template <int HALF>
+__device__ __forceinline__ uint64_t gt16(uint32_t a, uint32_t b) {
+    uint64_t m;
+    if (HALF == 0) asm("v_cmp_gt_i32_sdwa %0, sext(%1), sext(%2) src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(m) : "v"(a), "v"(b));
+    else asm("v_cmp_gt_i32_sdwa %0, sext(%1), sext(%2) src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(m) : "v"(a), "v"(b));
+    return m;
+}
+template <int HALF>
+__device__ __forceinline__ uint64_t eq16(uint32_t a, uint32_t b) {
+    uint64_t m;
+    if (HALF == 0) asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(m) : "v"(a), "v"(b));
+    else asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(m) : "v"(a), "v"(b));
+    return m;
+}
+__device__ __forceinline__ uint32_t rep16(int v) { return ((uint32_t)v & 0xFFFFu) | ((uint32_t)v << 16); }
+__device__ __forceinline__ int lo16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
+__device__ __forceinline__ int hi16(uint32_t x) { return (int)(int16_t)(x >> 16); }
+
+struct DualOut {
+    PassOut o[2];
+};
+
+struct DualIo {
+    const uint8_t* Q[2];
+    const uint8_t* T[2];
+    uint32_t* ptrs[2];
+    int32_t* B;  // packed boundary row (pair A's allocation)
+};
+
+// One pass of both pairs; see run_pass (ta_kernels.hip) for the shared structure.
+template <int MODE, bool CIGAR, int NV, bool QDASH>
+__device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
+                                             uint32_t pass, bool last_pass, bool tdash, int lane) {
+    constexpr int R = kRows;
+    constexpr bool LOCAL = MODE == kLocal;
+    const int ma = a.match, mi = a.mismatch, gap = a.gap;
+    const int init = (MODE == kGlobal) ? gap : 0;
+    const int zstep = 1 - 16 * ma;  // local: S(0, j) = zstep * j
+    const uint32_t KD = rep16(LOCAL ? 16 * (mi - ma) : (mi - ma));
+    const int glg = LOCAL ? 16 * gap + zstep : gap - ma;  // left gain, target byte != '-'
+    const int gld = LOCAL ? zstep : -ma;                  // left gain, target byte == '-'
+    const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : gap);  // up gain, query byte != '-'
+    const uint32_t GUD = rep16(LOCAL ? -1 : 0);
+    const uint32_t ONE = 0x00010001u;
+    const uint32_t Tmax = pass_steps(m);
+    const uint32_t row_base = pass * kPassRows;
+    const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
+    const uint32_t nl = (nrows + R - 1) / R;
+    const bool has_next = !last_pass;
+
+    uint32_t q2[R], H2[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i0 = row_base + (uint32_t)lane * R + r;
+        q2[r] = i0 < n ? ((uint32_t)io.Q[0][i0] | ((uint32_t)io.Q[1][i0] << 16)) : 0u;
+        H2[r] = rep16(LOCAL ? -(int)(i0 + 1) : wmul(i0 + 1, init));  // S(i, 0)
+    }
+    const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
+    uint32_t recv = rep16(LOCAL ? -(int)ia : wmul(ia, init));
+    uint32_t tc2 = 0;
+    const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
+    // local clamp base Zb = zstep*j - (ia + 1) for this lane's column j (= t - lane + 1)
+    int zb = zstep * (0 - lane) - (int)(ia + 1);  // value at t = -1
+    uint32_t bestK = 0xFFFFFFFFu;  // per half: signed -1 = no cell yet
+    uint32_t bestj = 0;
+    int rowbest[2] = {INT_MIN, INT_MIN};
+    uint32_t rowbest_j[2] = {0, 0};
+
+    uint32_t tcur[2], tnext[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        tcur[h] = load_tchunk(io.T[h], m, 0, lane);
+        tnext[h] = load_tchunk(io.T[h], m, 1, lane);
+    }
+    int bcur = 0, bnext = 0;
+    if (pass > 0) {
+        bcur = load_bchunk(io.B, m, 0, lane);
+        bnext = load_bchunk(io.B, m, 1, lane);
+    }
+    const uint32_t steps = m + nl - 1;
+    uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * Tmax * kWave : nullptr;
+    uint32_t* prow1 = CIGAR ? io.ptrs[1] + (uint64_t)pass * Tmax * kWave : nullptr;
+
+    auto step = [&](uint32_t t, auto masked_tag) {
+        constexpr bool MASKED = decltype(masked_tag)::value;
+        if ((t & 255u) == 0 && t) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                tcur[h] = tnext[h];
+                tnext[h] = load_tchunk(io.T[h], m, (t >> 8) + 1, lane);
+            }
+        }
+        uint32_t top;
+        if (pass == 0) {
+            top = rep16(LOCAL ? zstep * (int)(t + 1) : (init - ma) * (int)(t + 1));  // S(0, j)
+        } else {
+            if ((t & 63u) == 0 && t) {
+                bcur = bnext;
+                bnext = load_bchunk(io.B, m, (t >> 6) + 1, lane);
+            }
+            top = (uint32_t)rdlane(bcur, t & 63u);
+        }
+        const uint32_t sh = (t & 3u) * 8;
+        const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
+        const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
+        const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
+        const uint32_t prev = recv;
+        recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
+        tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        zb += zstep;
+
+        const int j = (int)t - lane + 1;
+        const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
+        uint32_t acc0 = 0, acc1 = 0;
+        if (active) {
+            uint32_t GL = rep16(glg);
+            if (tdash) {
+                const int ga = ((tc2 & 0xFFFFu) == '-') ? gld : glg;
+                const int gb = ((tc2 >> 16) == '-') ? gld : glg;
+                GL = ((uint32_t)ga & 0xFFFFu) | ((uint32_t)gb << 16);
+            }
+            auto e_of = [&](int r) { return pk_min_u16(q2[r] ^ tc2, ONE); };  // 0 on a match, 1 otherwise
+            uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
+            uint32_t upv = recv;
+            uint32_t Z = rep16(zb);
+            static_for<0, R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                const uint32_t old = H2[r];
+                const uint32_t diag = dnext;
+                const uint32_t left = pk_add(old, GL);
+                if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
+                uint32_t gu = GUG;
+                if (QDASH) {
+                    const uint32_t qd = q2[r];
+                    const uint32_t ua = ((qd & 0xFFFFu) == '-') ? GUD : GUG;
+                    const uint32_t ub = ((qd >> 16) == '-') ? GUD : GUG;
+                    gu = (ua & 0xFFFFu) | (ub & 0xFFFF0000u);
+                }
+                const uint32_t up = pk_add(upv, gu);
+                const uint32_t m1 = pk_max(diag, left);
+                uint32_t hv = pk_max(m1, up);
+                if (LOCAL) hv = pk_max(hv, Z);  // clamp, :185
+                if (CIGAR) {
+                    uint64_t hiA = gt16<0>(up, m1), hiB = gt16<1>(up, m1);
+                    const uint64_t iA = gt16<0>(left, diag), iB = gt16<1>(left, diag);
+                    uint64_t loA = iA & ~hiA, loB = iB & ~hiB;
+                    if (LOCAL) {
+                        const uint64_t sA = eq16<0>(hv, Z), sB = eq16<1>(hv, Z);
+                        hiA |= sA;
+                        loA |= sA;
+                        hiB |= sB;
+                        loB |= sB;
+                    }
+                    acc0 = shl1_add_lanebit(acc0, hiA);
+                    acc0 = shl1_add_lanebit(acc0, loA);
+                    acc1 = shl1_add_lanebit(acc1, hiB);
+                    acc1 = shl1_add_lanebit(acc1, loB);
+                }
+                H2[r] = hv;
+                upv = hv;
+                if (LOCAL && r + 1 < R) Z = pk_sub(Z, ONE);
+            });
+            if (LOCAL) {
+                // balanced trees (a serial packed-max chain stalls one cycle per link)
+                const uint32_t lo = tree_max<0, NV>(H2);
+                uint32_t sk = lo;
+                if (NV != R) {
+                    const uint32_t full = pk_max(lo, tree_max<NV, R>(H2));
+                    sk = ((uint32_t)lane == nl - 1) ? lo : full;
+                }
+                // key = S - Zbase + 15 = 16H + 15 - r (per half)
+                const uint32_t key = pk_add(pk_sub(sk, rep16(zb)), rep16(15));
+                const bool ua = lo16(key) > lo16(bestK), ub = hi16(key) > hi16(bestK);
+                const uint32_t keep = (ua ? 0u : 0xFFFFu) | (ub ? 0u : 0xFFFF0000u);
+                bestK = (bestK & keep) | (key & ~keep);
+                bestj = (bestj & keep) | (rep16(j) & ~keep);
+            }
+            if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + ma*j
+                const uint32_t v = H2[NV - 1];
+                const int va = lo16(v) + ma * j, vb = hi16(v) + ma * j;
+                if (va > rowbest[0]) {
+                    rowbest[0] = va;
+                    rowbest_j[0] = (uint32_t)j;
+                }
+                if (vb > rowbest[1]) {
+                    rowbest[1] = vb;
+                    rowbest_j[1] = (uint32_t)j;
+                }
+            }
+            if (has_next && (uint32_t)lane == nl - 1) io.B[j] = (int32_t)H2[R - 1];
+        }
+        if (CIGAR) {
+            prow0[t * kWave + lane] = acc0;
+            prow1[t * kWave + lane] = acc1;
+        }
+    };
+    const uint32_t ramp_end = min(nl - 1, steps);
+    uint32_t t = 0;
+    for (; t < ramp_end; ++t) step(t, std::true_type{});
+    for (; t < m; ++t) step(t, std::false_type{});
+    for (; t < steps; ++t) step(t, std::true_type{});
+
+    DualOut out;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        PassOut& o = out.o[h];
+        o = PassOut{INT_MIN, 0, 0, INT_MIN, 0, 0};
+        if (LOCAL) {
+            const int K = h ? hi16(bestK) : lo16(bestK);
+            const int v = ((uint32_t)lane >= nl || K < 0) ? -1 : (K >> 4);
+            const int mx = wave_max(v);
+            const int fl = first_lane(v == mx);
+            const int Kf = rdlane(K, fl);
+            const uint32_t jf = (uint32_t)rdlane((int)(h ? (bestj >> 16) : (bestj & 0xFFFFu)), fl);
+            o.h = mx;
+            o.i = row_base + (uint32_t)fl * R + (uint32_t)(15 - (Kf & 15)) + 1;
+            o.j = jf;
+        } else if (MODE == kSemi) {
+            // column m: H = S + ma*m for every row, so S orders them
+            int cv = INT_MIN;
+            uint32_t cr = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sv = h ? hi16(H2[r]) : lo16(H2[r]);
+                if ((uint32_t)r < nv_lane && sv > cv) {
+                    cv = sv;
+                    cr = r;
+                }
+            }
+            const int mx = wave_max(cv);
+            const int fl = first_lane(cv == mx && nv_lane > 0);
+            o.h = mx + ma * (int)m;
+            o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane((int)cr, fl) + 1;
+            o.j = m;
+            if (last_pass) {
+                o.row_h = rdlane(rowbest[h], nl - 1);
+                o.row_j = (uint32_t)rdlane((int)rowbest_j[h], nl - 1);
+            }
+        } else {
+            if (last_pass) {
+                int hv[R];
+#pragma unroll
+                for (int r = 0; r < R; ++r) hv[r] = h ? hi16(H2[r]) : lo16(H2[r]);
+                o.corner = rdlane(select_row<R>(hv, nrows - (nl - 1) * R - 1), nl - 1) + ma * (int)m;
+            }
+        }
+    }
+    return out;
+}
+
+template <int MODE, bool CIGAR, bool QDASH>
+__device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
+                                                uint32_t pass, bool last_pass, bool tdash, int lane) {
+    const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
+    const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
+    if (MODE == kGlobal || nv == kRows) return dual_pass<MODE, CIGAR, kRows, QDASH>(a, io, n, m, pass, last_pass, tdash, lane);
+#define TA_NV_CASE(k) \
+    case k: return dual_pass<MODE, CIGAR, k, QDASH>(a, io, n, m, pass, last_pass, tdash, lane);
+    switch (nv) {
+        TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
+        TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
+        default: TA_NV_CASE(15)
+    }
+#undef TA_NV_CASE
+}
+
+// dual_order: 2 pair ids per wave (both pairs have the same n and m and fit int16)
+template <int MODE, bool CIGAR>
+__global__ __launch_bounds__(kBlock) void dual_fill_kernel(FillArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t widx = wave_id();
+    if (widx >= a.count) return;
+    uint32_t p[2];
+    p[0] = a.order[2 * (a.begin + widx)];
+    p[1] = a.order[2 * (a.begin + widx) + 1];
+    const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
+    DualIo io;
+    bool tdash = false, qdash_any = false;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        io.Q[h] = a.qbytes + a.qoff[p[h]];
+        io.T[h] = a.tbytes + a.toff[p[h]];
+        io.ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
+        for (uint32_t k = (uint32_t)lane; k < m; k += 64) tdash |= io.T[h][k] == '-';
+    }
+    tdash = __ballot(tdash) != 0;
+    const uint32_t passes = n_passes(n);
+    io.B = (passes > 1) ? a.bnd + a.bnd_off[p[0]] : nullptr;
+    int best_h[2], corner[2] = {0, 0};
+    uint32_t best_i[2], best_j[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        best_h[h] = (MODE == kSemi) ? 0 : INT_MIN;
+        best_i[h] = 0;
+        best_j[h] = (MODE == kSemi) ? m : 0;
+    }
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        const bool last_pass = pass + 1 == passes;
+        bool dash = false;
+        const uint32_t row0 = pass * kPassRows + (uint32_t)lane * kRows;
+#pragma unroll
+        for (int r = 0; r < kRows; ++r)
+            dash |= (row0 + r < n) && (io.Q[0][row0 + r] == '-' || io.Q[1][row0 + r] == '-');
+        (void)qdash_any;
+        DualOut o;
+        if (__ballot(dash)) o = dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, pass, last_pass, tdash, lane);
+        else o = dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, pass, last_pass, tdash, lane);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (MODE != kGlobal && o.o[h].h > best_h[h]) {
+                best_h[h] = o.o[h].h;
+                best_i[h] = o.o[h].i;
+                best_j[h] = o.o[h].j;
+            }
+            if (MODE == kSemi && last_pass && o.o[h].row_h > best_h[h]) {
+                best_h[h] = o.o[h].row_h;
+                best_i[h] = n;
+                best_j[h] = o.o[h].row_j;
+            }
+            if (MODE == kGlobal && last_pass) corner[h] = o.o[h].corner;
+        }
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    }
+    if (CIGAR && a.fused) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t gi = (MODE == kGlobal) ? n : best_i[h], gj = (MODE == kGlobal) ? m : best_j[h];
+        if (CIGAR && a.fused) {
+            uint64_t st;
+            uint32_t len;
+            traceback_pair<MODE>(io.ptrs[h], n, m, gi, gj, a.slots + a.slot_off[p[h]], cigar_slot_bytes(n, m), lane,
+                                 &st, &len);
+            if (lane == 0) {
+                a.cigar_start[p[h]] = a.slot_off[p[h]] + st;
+                a.cigar_len[p[h]] = len;
+            }
+        }
+        if (lane == 0) {
+            a.score[p[h]] = (MODE == kGlobal) ? corner[h] : best_h[h];
+            a.target_begin[p[h]] = (MODE == kLocal) ? best_j[h] + 1 : 0;
+            a.goal_i[p[h]] = gi;
+            a.goal_j[p[h]] = gj;
+        }
+    }
+}
+
+inline dim3 dual_grid(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock); }
+
+#endif  // TA_DUAL_MODE
+}  // namespace
+
+#ifdef TA_DUAL_MODE
+template <>
+hipError_t launch_dual_mode<TA_DUAL_MODE, (TA_DUAL_CIGAR != 0)>(const FillArgs& a, hipStream_t s) {
+    if (!a.count) return hipSuccess;
+    hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, TA_DUAL_CIGAR != 0>), dual_grid(a.count), dim3(kBlock), 0, s,
+                       a);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace ta

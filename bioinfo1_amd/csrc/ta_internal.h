@@ -92,6 +92,12 @@ hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipSt
 template <int MODE, bool CIGAR>
 hipError_t launch_fill_mode(bool wide, const FillArgs& a, hipStream_t s);
 hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s);
+// Dual-pair packed int16 fill (ta_dual.hip): a.order holds 2 pair ids per wave.
+hipError_t launch_dual(int mode, bool cigar, const FillArgs& a, hipStream_t s);
+template <int MODE, bool CIGAR>
+hipError_t launch_dual_mode(const FillArgs& a, hipStream_t s);
+// Can an n x m pair run in the packed int16 kernel without overflow?
+bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 
 }  // namespace ta

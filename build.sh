@@ -3,7 +3,7 @@
 # in-tree, and the test-only oracle libraries.  Used by __graft_entry__.build().
 # ta_kernels.hip is compiled once per (fill mode, cigar) pair (TA_FILL_MODE,
 # TA_FILL_CIGAR) and once for the traceback/compact kernels (TA_TU_MISC), in
-# parallel.
+# parallel; ta_dual.hip (packed two-pair fill) likewise per (mode, cigar).
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")" && pwd)"
 CS="$ROOT/bioinfo1_amd/csrc"
@@ -16,12 +16,13 @@ pids=()
 for m in 0 1 2; do
   for c in 0 1; do
     "$HIPCC" "${FLAGS[@]}" -DTA_FILL_MODE=$m -DTA_FILL_CIGAR=$c -c "$CS/ta_kernels.hip" -o "$B/ta_fill_$m$c.o" & pids+=($!)
+    "$HIPCC" "${FLAGS[@]}" -DTA_DUAL_MODE=$m -DTA_DUAL_CIGAR=$c -c "$CS/ta_dual.hip" -o "$B/ta_dual_$m$c.o" & pids+=($!)
   done
 done
 "$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$CS/ta_kernels.hip" -o "$B/ta_misc.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip" -o "$B/ta_api.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp" -o "$B/shim.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_api.o" "$B/shim.o" -o "$OUT"
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_api.o" "$B/shim.o" -o "$OUT"
 make -s -C "$ROOT/oracle" >/dev/null
 echo "built $OUT"

@@ -94,6 +94,9 @@ uint64_t ta_plan_cigar_slots_bytes(const ta_plan* plan);
 /* Device workspace held by the plan, and the number of launch chunks. */
 uint64_t ta_plan_workspace_bytes(const ta_plan* plan);
 uint32_t ta_plan_chunks(const ta_plan* plan);
+/* Pairs the plan runs in the packed two-pairs-per-wave int16 kernel (equal
+ * lengths, scores provably within int16); the rest use the int32 kernel. */
+uint32_t ta_plan_dual_pairs(const ta_plan* plan);
 
 /* Device pointers for one execution of a plan. */
 typedef struct ta_device_io {

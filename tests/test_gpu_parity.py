@@ -106,6 +106,53 @@ def test_oracle_fuzz(aligner, oracle, case):
             int(want.scores[p]), want.cigar(p), int(want.target_begins[p])), (case, p, b.qlen[p], b.tlen[p])
 
 
+# Batches whose pairs repeat a few (n, m) shapes, so most of them couple into
+# the packed two-pair int16 fill (ta_dual.hip): (mode, scoring, alphabet, shapes, n_pairs)
+DUAL_FUZZ = [
+    (0, (1, -1, -1), b"ACGT", [(1, 1), (1, 5), (7, 3), (16, 16), (17, 200), (64, 64), (100, 37)], 300),
+    (1, (1, -1, -1), b"ACGT", [(1, 1), (1, 5), (7, 3), (16, 16), (17, 200), (64, 64), (100, 37)], 300),
+    (2, (1, -1, -1), b"ACGT", [(1, 1), (1, 5), (7, 3), (16, 16), (17, 200), (64, 64), (100, 37)], 300),
+    (0, (2, -1, 2), b"AC-GT", [(33, 90), (250, 250), (5, 300)], 120),
+    (1, (2, -1, 2), b"AC-GT", [(33, 90), (250, 250), (5, 300)], 120),
+    (2, (2, -1, 2), b"AC-GT", [(33, 90), (250, 250), (5, 300)], 120),
+    (1, (5, -4, -3), b"acgtN-", [(300, 280), (31, 31)], 80),
+    (2, (3, -2, 0), b"ACGT-", [(300, 280), (31, 31)], 80),
+    (0, (1, -1, -1), b"ACGT", [(1024, 1024), (1025, 700), (1500, 1500), (2100, 900)], 24),
+    (1, (1, -1, -1), b"ACGT", [(1024, 1024), (1025, 700), (1500, 1500), (1900, 1900)], 24),
+    (2, (1, -1, -1), b"AC", [(1024, 1024), (1025, 700), (1500, 1500), (2100, 900)], 24),
+    (1, (1, 2, -3), b"AC", [(1017, 333), (2049, 64)], 12),
+]
+
+
+def _shaped_batch(P, shapes, alphabet, seed):
+    rng = np.random.default_rng(seed)
+    al = np.frombuffer(alphabet, np.uint8)
+    pairs = []
+    for k in range(P):
+        n, m = shapes[rng.integers(len(shapes))]
+        pairs.append((al[rng.integers(len(al), size=n)].tobytes(), al[rng.integers(len(al), size=m)].tobytes()))
+    return synth.from_pairs(pairs)
+
+
+@pytest.mark.parametrize("case", range(len(DUAL_FUZZ)))
+def test_dual_fuzz(aligner, oracle, case, monkeypatch):
+    mode, sc, alpha, shapes, P = DUAL_FUZZ[case]
+    b = _shaped_batch(P, shapes, alpha, 0xD0A1 + case)
+    plan = DevicePlan(aligner, b, mode, *sc, True)
+    assert plan.dual_pairs >= P // 2, plan.dual_pairs
+    plan.close()
+    want = oracle.align_batch(b, mode, *sc, True)
+    for dual in ("1", "0"):
+        monkeypatch.setenv("TA_DUAL", dual)
+        for cig in (True, False):
+            got = aligner.align_batch(b, mode, *sc, cig)
+            np.testing.assert_array_equal(got.scores, want.scores)
+            np.testing.assert_array_equal(got.target_begins, want.target_begins)
+            if cig:
+                for p in range(P):
+                    assert got.cigar(p) == want.cigar(p), (case, dual, p, b.qlen[p], b.tlen[p])
+
+
 def test_related_long_pairs(aligner, oracle):
     # long tracebacks across pass and tile boundaries
     for mode in (0, 1, 2):
@@ -123,7 +170,9 @@ def test_device_plan_and_chunking(aligner):
     host = aligner.align_batch(b, 1, 1, -1, -1, True)
     for budget in (0, 3 * 1063 * 256):  # default, and ~3 pairs per chunk
         plan = DevicePlan(aligner, b, 1, 1, -1, -1, True, workspace_budget=budget)
-        assert plan.chunks == (1 if budget == 0 else 100)
+        # couples of equal-shape pairs share a wave (dual fill): 2 pairs per chunk then
+        per_chunk = 2 if plan.dual_pairs == b.n_pairs else 3
+        assert plan.chunks == (1 if budget == 0 else -(-b.n_pairs // per_chunk))
         plan.run()
         torch.cuda.synchronize()
         r = plan.results()
