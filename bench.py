@@ -163,7 +163,7 @@ def main():
     stream = torch.cuda.current_stream(dev)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo: host tensors
     rec = torch.zeros((3, P), dtype=torch.int32, device=coll_dev)
-    gathered = torch.zeros((world, 3, P), dtype=torch.int32, device=coll_dev) if world > 1 else None
+    gathered = torch.zeros((world * 3, P), dtype=torch.int32, device=coll_dev) if world > 1 else None
 
     def step():
         plan.run()

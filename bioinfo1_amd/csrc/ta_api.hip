@@ -52,6 +52,7 @@ struct ta_plan {
     uint32_t *d_goal_i = nullptr, *d_goal_j = nullptr;
     uint32_t* d_ptrs = nullptr;
     int32_t* d_bnd = nullptr;
+    uint32_t* d_fb = nullptr;  // dual fallback: [n_dual_pairs] list, then one counter per chunk
 };
 
 namespace {
@@ -147,7 +148,7 @@ void ta_plan_destroy(ta_plan* pl) {
     (void)hipSetDevice(pl->ctx->device);
     for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_ptr_off,
                     (void*)pl->d_bnd_off, (void*)pl->d_slot_off, (void*)pl->d_goal_i, (void*)pl->d_goal_j,
-                    (void*)pl->d_ptrs, (void*)pl->d_bnd})
+                    (void*)pl->d_ptrs, (void*)pl->d_bnd, (void*)pl->d_fb})
         if (p) (void)hipFree(p);
     delete pl;
 }
@@ -258,6 +259,9 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
         rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc pointer workspace");
     if (rc == TA_OK && pl->ws_bnd_words && hipMalloc(&pl->d_bnd, pl->ws_bnd_words * 4ull) != hipSuccess)
         rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc boundary workspace");
+    if (rc == TA_OK && pl->n_dual_pairs &&
+        hipMalloc(&pl->d_fb, (pl->n_dual_pairs + pl->chunks.size()) * 4ull) != hipSuccess)
+        rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc dual fallback list");
     if (rc != TA_OK) {
         ta_plan_destroy(pl);
         return rc;
@@ -307,7 +311,18 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
             d.order = pl->d_duals;
             d.begin = ch.dbegin;
             d.count = ch.dcount;
+            d.fb_list = pl->d_fb + 2ull * ch.dbegin;
+            d.fb_count = pl->d_fb + pl->n_dual_pairs + c;
+            TA_HIP(pl->ctx, hipMemsetAsync(d.fb_count, 0, 4, s));
             TA_HIP(pl->ctx, ta::launch_dual(pl->type, pl->want_cigar, d, s));
+            // couples the dual kernel handed back ('-' in a query): int32 fill,
+            // wave count read on the device (grid sized for all of them)
+            ta::FillArgs f = a;
+            f.order = d.fb_list;
+            f.begin = 0;
+            f.count = 2 * ch.dcount;
+            f.count_dev = d.fb_count;
+            TA_HIP(pl->ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, f, s));
         }
         if (ch.scount) {
             a.order = pl->d_singles;

@@ -84,7 +84,7 @@ struct DualIo {
 };
 
 // One pass of both pairs; see run_pass (ta_kernels.hip) for the shared structure.
-template <int MODE, bool CIGAR, int NV, bool QDASH>
+template <int MODE, bool CIGAR, int NV>
 __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
                                              uint32_t pass, bool last_pass, bool tdash, int lane) {
     constexpr int R = kRows;
@@ -95,8 +95,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     const uint32_t KD = rep16(LOCAL ? 16 * (mi - ma) : (mi - ma));
     const int glg = LOCAL ? 16 * gap + zstep : gap - ma;  // left gain, target byte != '-'
     const int gld = LOCAL ? zstep : -ma;                  // left gain, target byte == '-'
-    const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : gap);  // up gain, query byte != '-'
-    const uint32_t GUD = rep16(LOCAL ? -1 : 0);
+    const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : gap);  // up gain (no '-' in these queries)
     const uint32_t ONE = 0x00010001u;
     const uint32_t Tmax = pass_steps(m);
     const uint32_t row_base = pass * kPassRows;
@@ -185,14 +184,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 const uint32_t diag = dnext;
                 const uint32_t left = pk_add(old, GL);
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
-                uint32_t gu = GUG;
-                if (QDASH) {
-                    const uint32_t qd = q2[r];
-                    const uint32_t ua = ((qd & 0xFFFFu) == '-') ? GUD : GUG;
-                    const uint32_t ub = ((qd >> 16) == '-') ? GUD : GUG;
-                    gu = (ua & 0xFFFFu) | (ub & 0xFFFF0000u);
-                }
-                const uint32_t up = pk_add(upv, gu);
+                const uint32_t up = pk_add(upv, GUG);
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv = pk_max(m1, up);
                 if (LOCAL) hv = pk_max(hv, Z);  // clamp, :185
@@ -304,14 +296,14 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     return out;
 }
 
-template <int MODE, bool CIGAR, bool QDASH>
+template <int MODE, bool CIGAR>
 __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
                                                 uint32_t pass, bool last_pass, bool tdash, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
-    if (MODE == kGlobal || nv == kRows) return dual_pass<MODE, CIGAR, kRows, QDASH>(a, io, n, m, pass, last_pass, tdash, lane);
+    if (MODE == kGlobal || nv == kRows) return dual_pass<MODE, CIGAR, kRows>(a, io, n, m, pass, last_pass, tdash, lane);
 #define TA_NV_CASE(k) \
-    case k: return dual_pass<MODE, CIGAR, k, QDASH>(a, io, n, m, pass, last_pass, tdash, lane);
+    case k: return dual_pass<MODE, CIGAR, k>(a, io, n, m, pass, last_pass, tdash, lane);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -321,8 +313,14 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
 }
 
 // dual_order: 2 pair ids per wave (both pairs have the same n and m and fit int16)
+// 5 waves/SIMD: local+CIGAR needs ~105 VGPRs unconstrained (occupancy 4); at
+// 96 the allocator spills two pass-invariant pointers, reloaded off the
+// per-cell path.
+#ifndef TA_DUAL_WAVES
+#define TA_DUAL_WAVES 5
+#endif
 template <int MODE, bool CIGAR>
-__global__ __launch_bounds__(kBlock) void dual_fill_kernel(FillArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t widx = wave_id();
     if (widx >= a.count) return;
@@ -331,13 +329,25 @@ __global__ __launch_bounds__(kBlock) void dual_fill_kernel(FillArgs a) {
     p[1] = a.order[2 * (a.begin + widx) + 1];
     const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
     DualIo io;
-    bool tdash = false, qdash_any = false;
+    bool tdash = false, qdash = false;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         io.Q[h] = a.qbytes + a.qoff[p[h]];
         io.T[h] = a.tbytes + a.toff[p[h]];
         io.ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
         for (uint32_t k = (uint32_t)lane; k < m; k += 64) tdash |= io.T[h][k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < n; k += 64) qdash |= io.Q[h][k] == '-';
+    }
+    // A '-' in a query changes the up gain per row; that variant would cost
+    // this kernel ~30 VGPRs for input real reads never contain, so such
+    // couples go to the int32 fill (launched right after, same workspace).
+    if (__ballot(qdash)) {
+        if (lane == 0) {
+            const uint32_t at = atomicAdd(a.fb_count, 2u);
+            a.fb_list[at] = p[0];
+            a.fb_list[at + 1] = p[1];
+        }
+        return;
     }
     tdash = __ballot(tdash) != 0;
     const uint32_t passes = n_passes(n);
@@ -352,15 +362,7 @@ __global__ __launch_bounds__(kBlock) void dual_fill_kernel(FillArgs a) {
     }
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const bool last_pass = pass + 1 == passes;
-        bool dash = false;
-        const uint32_t row0 = pass * kPassRows + (uint32_t)lane * kRows;
-#pragma unroll
-        for (int r = 0; r < kRows; ++r)
-            dash |= (row0 + r < n) && (io.Q[0][row0 + r] == '-' || io.Q[1][row0 + r] == '-');
-        (void)qdash_any;
-        DualOut o;
-        if (__ballot(dash)) o = dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, pass, last_pass, tdash, lane);
-        else o = dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, pass, last_pass, tdash, lane);
+        const DualOut o = dual_pass_nv<MODE, CIGAR>(a, io, n, m, pass, last_pass, tdash, lane);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (MODE != kGlobal && o.o[h].h > best_h[h]) {

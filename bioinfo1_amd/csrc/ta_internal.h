@@ -60,6 +60,11 @@ struct FillArgs {
     const uint64_t* slot_off;
     uint64_t* cigar_start;
     uint32_t* cigar_len;
+    // dual fill: couples with a '-' query byte are handed to the int32 fill
+    // through this list; that launch reads its wave count from count_dev
+    uint32_t* fb_list;
+    uint32_t* fb_count;
+    const uint32_t* count_dev;
 };
 
 struct TraceArgs {

@@ -328,7 +328,7 @@ template <int MODE, bool CIGAR, bool WIDE>
 __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t widx = wave_id();
-    if (widx >= a.count) return;  // wave-uniform
+    if (widx >= (a.count_dev ? *a.count_dev : a.count)) return;  // wave-uniform
     const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
     const uint32_t n = a.qlen[p], m = a.tlen[p];
     if (n == 0 || m == 0) {
