@@ -23,10 +23,11 @@ def asm_text(path=None):
     out = "/tmp/ta_census"
     os.makedirs(out, exist_ok=True)
     extra = os.environ.get("TA_CENSUS_FLAGS", "-DTA_FILL_MODE=1 -DTA_FILL_CIGAR=1").split()
+    src = os.environ.get("TA_CENSUS_SRC", "ta_kernels")  # or ta_dual (with -DTA_DUAL_MODE=.. -DTA_DUAL_CIGAR=..)
     subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", *extra, "-c",
-                           os.path.join(ROOT, "bioinfo1_amd/csrc/ta_kernels.hip"), "-o", f"{out}/k.o", "-save-temps"],
+                           os.path.join(ROOT, f"bioinfo1_amd/csrc/{src}.hip"), "-o", f"{out}/k.o", "-save-temps"],
                           cwd=out, stderr=subprocess.DEVNULL)
-    return open(f"{out}/ta_kernels-hip-amdgcn-amd-amdhsa-gfx950.s").read()
+    return open(f"{out}/{src}-hip-amdgcn-amd-amdhsa-gfx950.s").read()
 
 
 def classify(op):

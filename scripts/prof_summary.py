@@ -55,7 +55,9 @@ def main():
         json.dump(pmc, fh, indent=1)
     fill = {k: v for k, v in pmc.items() if "fill_kernel" in k}
     if fill:
-        k, cs = next(iter(fill.items()))
+        # the dominant fill launch (dual and int32 fills both match; the int32
+        # one may be the near-empty fallback launch for '-' queries)
+        k, cs = max(fill.items(), key=lambda kv: kv[1].get("SQ_INSTS_VALU", 0))
         tr = None
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             tr = int((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024)
