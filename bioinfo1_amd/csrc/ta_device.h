@@ -147,7 +147,6 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
     // bounds (and the pass) need checking.
     uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tL0 = 0;
     uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
-    const int lane2 = 2 * lane;
     while (true) {
         if (MODE == kLocal) {
             if ((i == 0) | (j == 0)) break;  // row/col 0 cost 0 ends the walk (:202)
@@ -183,25 +182,29 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
         const uint32_t comp = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
         const uint32_t kk = t - tt0;
         const uint32_t dw = (uint32_t)rdlane((int)comp, kk);
-        const uint32_t fld = 30u - 2u * r;  // bit offset of row r's 2-bit code
-        const uint32_t code = (dw >> fld) & 3u;
-        if (code == kCodeStop) break;  // local: cost == 0 (:202)
+        // bit planes (ta_internal.h Code): row r's D bit at 31 - r, I bit at 15 - r
+        const uint32_t sh = 15u - r;
+        const uint32_t dbit = (dw >> (sh + kDPlane)) & 1u, ibit = (dw >> sh) & 1u;
+        if (MODE == kLocal && (dbit & ibit)) break;  // STOP: cost == 0 (:202)
         uint32_t run;
-        if (code == kCodeD) {
-            const uint32_t x = (dw ^ 0xAAAAAAAAu) >> fld;  // D fields of rows r, r-1, .. become 00
-            run = x ? ((uint32_t)__ffs((int)x) - 1u) >> 1 : 16u;
-            run = min(run, r + 1u);
+        if (dbit) {
+            // D cells of rows r, r-1, ..: the D plane (local: minus STOP cells)
+            // shifted so that row r is bit 0; the run is its trailing ones
+            uint32_t dp = dw >> kDPlane;
+            if (MODE == kLocal) dp &= ~dw;
+            run = (uint32_t)__builtin_ctz(~((dp & 0xFFFFu) >> sh));  // <= r + 1
             w.push('D', run);
             i -= run;
-        } else if (code == kCodeI) {
-            const uint32_t v = __builtin_amdgcn_ubfe(comp, fld, 2u);  // row r at every step of the tile
-            run = min(streak_down(ballot(v == kCodeI), kk), j);
+        } else if (ibit) {
+            // row r at every step of the tile: I code = I bit set, D bit clear
+            const uint32_t v = (comp >> sh) & 0x10001u;
+            run = min(streak_down(ballot(v == 1u), kk), j);
             w.push('I', run);
             j -= run;
         } else {
-            // diagonal: step tt0+lane holds row r - (kk - lane), bit offset fld + 2*(kk - lane)
-            const uint32_t v = __builtin_amdgcn_ubfe(comp, (uint32_t)((int)(fld + 2u * kk) - lane2), 2u);
-            run = min(min(streak_down(ballot(v == kCodeM), kk), r + 1u), j);
+            // diagonal: step tt0+lane holds row r - (kk - lane), i.e. shift sh + (kk - lane)
+            const uint32_t v = (comp >> ((sh + kk - (uint32_t)lane) & 31u)) & 0x10001u;
+            run = min(min(streak_down(ballot(v == 0u), kk), r + 1u), j);
             w.push('M', run);
             i -= run;
             j -= run;

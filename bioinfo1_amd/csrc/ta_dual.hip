@@ -13,9 +13,11 @@
 //      is the reference's row-major first-max key; the clamp H >= 0 becomes
 //      S >= (1-16ma)j - i, a per-lane-per-step base minus the row index)
 // A cell's inputs move exactly as in fill_kernel (lane skew, DPP wave_shr:1).
-// Compares for the pointer codes are per half (SDWA word selects); the lane
-// masks are canonicalised on the SALU and shifted into one dword per pair
-// per lane per step with v_addc, exactly like the int32 kernel.
+// The pointer codes never leave the VALU: each compare is the sign of a
+// saturating packed subtraction, v_perm_b32 spreads the sign bits of both
+// pairs to bytes and v_bfi_b32 inserts them into two row-group accumulators,
+// which two more v_perm_b32 per step turn into the per-pair bit-plane dwords
+// of ta_internal.h (Code).  No lane masks, no SALU, no v_addc chains.
 #include "ta_device.h"
 
 namespace ta {
@@ -41,32 +43,38 @@ __device__ __forceinline__ uint32_t tree_max(const uint32_t* v) {
     if constexpr (E - B == 1) return v[B];
     else return pk_max(tree_max<B, (B + E) / 2>(v), tree_max<(B + E) / 2, E>(v));
 }
-// hipcc does not form these two from vector C++ (it expands min(x,1) into
-// compares + selects), so they are spelled out.
+// Packed helpers through clang vector builtins (inline asm costs an s_nop:
+// the hazard recognizer cannot see into it).  pk_min_u16 must get a
+// non-constant operand: min(x, 1) with a literal 1 is expanded into compares.
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+typedef short s2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_pk_min_u16 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u2, a), __builtin_bit_cast(u2, b)));
 }
+// a * b + c per half (v_pk_mad_u16: the low 16 bits are the same as i16)
 __device__ __forceinline__ uint32_t pk_mad_i16(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2v, a) * __builtin_bit_cast(s2v, b) + __builtin_bit_cast(s2v, c));
+}
+// a - b per half, saturating (v_pk_sub_i16 clamp): its sign bits (15, 31) are the per-half a < b
+__device__ __forceinline__ uint32_t pk_sub_sat(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s2v, a), __builtin_bit_cast(s2v, b)));
+}
+// Pointer bits without lane masks: the sign bits of two compare words are
+// spread to whole bytes by v_perm_b32 (selectors 8..11 replicate the sign of
+// bytes 1, 3, 5, 7), giving [I_A, I_B, D_A, D_B] as 0x00/0xFF bytes, and one
+// bit-insert (v_bitop3_b32 on gfx950) drops them into bit (7 - r%8) of the
+// row group's accumulator.  The local-mode canonicalisation is two more
+// v_bitop3_b32, which hipcc forms from the logic expressions.
+constexpr uint32_t kSignBytes = 0x0B0A0908u;
+__device__ __forceinline__ uint32_t sign_bytes(uint32_t dword_d, uint32_t dword_i) {
+    return __builtin_amdgcn_perm(dword_d, dword_i, kSignBytes);
+}
+// v_bfi_b32 spelled out: from the C++ form hipcc builds and/or trees over
+// all 8 rows of a group, which keeps their sign bytes live (spills at 5 waves)
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
     uint32_t r;
-    asm("v_pk_mad_i16 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
     return r;
-}
-// per-half signed compares -> wave lane masks (one SDWA compare each)
-template <int HALF>
-__device__ __forceinline__ uint64_t gt16(uint32_t a, uint32_t b) {
-    uint64_t m;
-    if (HALF == 0) asm("v_cmp_gt_i32_sdwa %0, sext(%1), sext(%2) src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(m) : "v"(a), "v"(b));
-    else asm("v_cmp_gt_i32_sdwa %0, sext(%1), sext(%2) src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(m) : "v"(a), "v"(b));
-    return m;
-}
-template <int HALF>
-__device__ __forceinline__ uint64_t eq16(uint32_t a, uint32_t b) {
-    uint64_t m;
-    if (HALF == 0) asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_0 src1_sel:WORD_0" : "=s"(m) : "v"(a), "v"(b));
-    else asm("v_cmp_eq_u32_sdwa %0, %1, %2 src0_sel:WORD_1 src1_sel:WORD_1" : "=s"(m) : "v"(a), "v"(b));
-    return m;
 }
 __device__ __forceinline__ uint32_t rep16(int v) { return ((uint32_t)v & 0xFFFFu) | ((uint32_t)v << 16); }
 __device__ __forceinline__ int lo16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
@@ -96,7 +104,8 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     const int glg = LOCAL ? 16 * gap + zstep : gap - ma;  // left gain, target byte != '-'
     const int gld = LOCAL ? zstep : -ma;                  // left gain, target byte == '-'
     const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : gap);  // up gain (no '-' in these queries)
-    const uint32_t ONE = 0x00010001u;
+    uint32_t ONE = 0x00010001u;
+    asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16 (see pk_min_u16)
     const uint32_t Tmax = pass_steps(m);
     const uint32_t row_base = pass * kPassRows;
     const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
@@ -166,6 +175,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
 
         const int j = (int)t - lane + 1;
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
+        // rows 0-7 / 8-15: bytes [I_A, I_B, D_A, D_B], row r at bit 7 - r%8
         uint32_t acc0 = 0, acc1 = 0;
         if (active) {
             uint32_t GL = rep16(glg);
@@ -186,23 +196,19 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
                 const uint32_t up = pk_add(upv, GUG);
                 const uint32_t m1 = pk_max(diag, left);
-                uint32_t hv = pk_max(m1, up);
-                if (LOCAL) hv = pk_max(hv, Z);  // clamp, :185
+                const uint32_t u = pk_max(m1, up);
+                const uint32_t hv = LOCAL ? pk_max(u, Z) : u;  // clamp, :185
                 if (CIGAR) {
-                    uint64_t hiA = gt16<0>(up, m1), hiB = gt16<1>(up, m1);
-                    const uint64_t iA = gt16<0>(left, diag), iB = gt16<1>(left, diag);
-                    uint64_t loA = iA & ~hiA, loB = iB & ~hiB;
+                    uint32_t wd = pk_sub_sat(m1, up);    // sign: up > max(diag, left)  (DELETE)
+                    uint32_t wi = pk_sub_sat(diag, left);  // sign: left > diag           (INSERT)
                     if (LOCAL) {
-                        const uint64_t sA = eq16<0>(hv, Z), sB = eq16<1>(hv, Z);
-                        hiA |= sA;
-                        loA |= sA;
-                        hiB |= sB;
-                        loB |= sB;
+                        // canonical codes: D | S and (I & !D) | S, S = clamped to 0
+                        const uint32_t wn = pk_sub_sat(Z, u);  // sign: u > 0 (not STOP)
+                        wi = (wi & ~wd) | ~wn;
+                        wd = wd | ~wn;
                     }
-                    acc0 = shl1_add_lanebit(acc0, hiA);
-                    acc0 = shl1_add_lanebit(acc0, loA);
-                    acc1 = shl1_add_lanebit(acc1, hiB);
-                    acc1 = shl1_add_lanebit(acc1, loB);
+                    uint32_t& acc = (r < 8) ? acc0 : acc1;
+                    acc = bfi(0x01010101u << (7 - (r & 7)), sign_bytes(wd, wi), acc);
                 }
                 H2[r] = hv;
                 upv = hv;
@@ -238,8 +244,9 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             if (has_next && (uint32_t)lane == nl - 1) io.B[j] = (int32_t)H2[R - 1];
         }
         if (CIGAR) {
-            prow0[t * kWave + lane] = acc0;
-            prow1[t * kWave + lane] = acc1;
+            // per pair: [I rows 8-15, I rows 0-7, D rows 8-15, D rows 0-7] (ta_internal.h Code)
+            prow0[t * kWave + lane] = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
+            prow1[t * kWave + lane] = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
         }
     };
     const uint32_t ramp_end = min(nl - 1, steps);

@@ -18,8 +18,14 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 
 enum Mode : int { kGlobal = 0, kLocal = 1, kSemi = 2 };
 
-// 2-bit traceback code per cell (packed 16 rows per dword, row 0 in bits 31:30).
+// 2-bit traceback code per cell, code = (D bit << 1) | I bit.  One dword per
+// (pass, step, lane) holds the 16 rows of the lane's stripe as two bit
+// planes: D plane in bits 31:16 (row r at bit 31 - r), I plane in bits 15:0
+// (row r at bit 15 - r).  Local mode stores canonical codes (M=00 I=01 D=10
+// STOP=11); global / semi-global store the raw compares (up > max(diag,left),
+// left > diag), so there D wins whenever its bit is set (10 and 11 are D).
 enum Code : uint32_t { kCodeM = 0, kCodeI = 1, kCodeD = 2, kCodeStop = 3 };
+constexpr int kDPlane = 16;  // bit offset of the D plane
 
 // Steps of one pass over an m-column target: m + 63 (lane skew).
 __host__ __device__ inline uint32_t pass_steps(uint32_t m) { return m + kWave - 1; }

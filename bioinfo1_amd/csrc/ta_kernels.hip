@@ -164,7 +164,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
 
         const int j = (int)t - lane + 1;
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
-        uint32_t acc = 0;
+        uint32_t accD = 0, accI = 0;  // the two bit planes (ta_internal.h Code)
         if (active) {
             const int gt = (tc == '-') ? 0 : GTG;  // indel(t[j-1])
 #pragma unroll
@@ -192,19 +192,20 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
                 if (MODE == kLocal) h = SCALED ? max3_imm<R - r>(m1, up) : max3_imm<0>(m1, up);  // clamp, :185
                 else h = max(m1, up);
                 if (CIGAR) {
-                    // wave-wide lane masks from the VALU compares; the
-                    // canonical code is formed on the SALU:
-                    //   hi = D | S,  lo = (I & !D) | S   (M=00 I=01 D=10 STOP=11)
+                    // wave-wide lane masks from the VALU compares, shifted
+                    // into the D and I planes (row 0 ends up in bit 15).
+                    // Local mode canonicalises on the SALU:
+                    //   D = D | S,  I = (I & !D) | S   (M=00 I=01 D=10 STOP=11)
                     const uint64_t mD = ballot(up > m1);      // DELETE only if strictly greater
                     const uint64_t mI = ballot(left > diag);  // INSERT beats MATCH only if strictly greater
-                    uint64_t hi = mD, lo = mI & ~mD;
+                    uint64_t hi = mD, lo = mI;
                     if (MODE == kLocal) {
                         const uint64_t mS = ballot(h == (SCALED ? (R - r) : 0));  // cost 0 ends the walk
                         hi |= mS;
-                        lo |= mS;
+                        lo = (mI & ~mD) | mS;
                     }
-                    acc = shl1_add_lanebit(acc, hi);
-                    acc = shl1_add_lanebit(acc, lo);
+                    accD = shl1_add_lanebit(accD, hi);
+                    accI = shl1_add_lanebit(accI, lo);
                 }
                 if (MODE == kLocal && WIDE) {
                     if ((uint32_t)r < nv_lane && (h > bh || (h == bh && (uint32_t)r < br))) {
@@ -238,7 +239,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
             }
             if (has_next && (uint32_t)lane == nl - 1) B[j] = H[R - 1];
         }
-        if (CIGAR) prow[t * kWave + lane] = acc;
+        if (CIGAR) prow[t * kWave + lane] = (accD << kDPlane) | accI;
     };
     // lanes 0..nl-1 are all active for t in [nl-1, m-1]
     const uint32_t ramp_end = min(nl - 1, steps);

@@ -57,7 +57,7 @@ def main():
     f = [x for x in funcs if x.split(":")[0].find(sub) >= 0 and "s_endpgm" in x]
     if not f:
         sys.exit(f"no kernel matching {sub}")
-    body = f[0].split("s_endpgm")[0]
+    body = f[0].split(".Lfunc_end")[0]  # whole kernel (it may hold several s_endpgm)
     lines = body.splitlines()
     labels = {}
     for k, ln in enumerate(lines):
@@ -71,17 +71,26 @@ def main():
             tgt = m.group(1) or m.group(2)
             if tgt in labels and labels[tgt] < k:
                 loops.append((labels[tgt], k))
-    # innermost: loops that contain no other loop
-    inner = [l for l in loops if not any(o != l and l[0] <= o[0] and o[1] <= l[1] for o in loops)]
     print(f"{f[0].split(':')[0][:90]}")
-    for a, b in sorted(set(inner)):
+    # DP step loops: one step = 2 DPP moves (the wave_shr:1 hand-offs); static
+    # counts include the rarely taken chunk-load branches
+    seen = set()
+    for a, b in sorted(set(loops)):
         c = collections.Counter()
         for ln in lines[a:b + 1]:
             t = ln.strip().split()
             if t and not t[0].startswith((".", ";")) and not t[0].endswith(":"):
                 c[classify(t[0])] += 1
+        steps = c["DPP"] // 2
+        if steps == 0 or (c["DPP"], c["VALU"]) in seen:
+            continue
+        seen.add((c["DPP"], c["VALU"]))
         tot = sum(c.values())
-        print(f"  loop lines {a}-{b}: total {tot}  " + "  ".join(f"{k}={v}" for k, v in c.most_common()))
+        nop = sum(1 for ln in lines[a:b + 1] if ln.strip().startswith("s_nop"))
+        mov = sum(1 for ln in lines[a:b + 1] if ln.strip().startswith("v_mov_b32_e32"))
+        print(f"  step loop lines {a}-{b}: {steps} step(s), per step: VALU={c['VALU'] / steps:.1f} "
+              f"SALU={c['SALU'] / steps:.1f} VMEM={c['VMEM'] / steps:.1f} total={tot / steps:.1f} "
+              f"(s_nop={nop / steps:.1f} v_mov={mov / steps:.1f})")
 
 
 if __name__ == "__main__":
