@@ -33,7 +33,11 @@ struct ta_plan {
     uint32_t n_pairs = 0;
     int type = 0, match = 0, mismatch = 0, gap = 0;
     bool want_cigar = false, wide = false;
-    bool fused = true;  // traceback inside the fill kernel (TA_FUSED_TRACEBACK=0 disables)
+    // Traceback inside the fill kernel (TA_FUSED_TRACEBACK=0 disables).  Only
+    // for plans without dual couples: a dual wave would walk its two pairs one
+    // after the other, all waves at once after the fill; the separate
+    // traceback kernel walks every pair on its own wave (measured faster).
+    bool fused = true;
     bool dual = true;   // packed two-pair int16 fill where it fits (TA_DUAL=0 disables)
     std::vector<uint32_t> qlen, tlen, order, singles, duals;
     std::vector<uint64_t> slot_off;
@@ -233,6 +237,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
         k += units;
     }
     if (cur.count) pl->chunks.push_back(cur);
+    if (pl->n_dual_pairs) pl->fused = false;
     for (auto& c : pl->chunks) {
         pl->ws_ptr_dwords = std::max(pl->ws_ptr_dwords, c.ptr_dwords);
         pl->ws_bnd_words = std::max(pl->ws_bnd_words, c.bnd_words);

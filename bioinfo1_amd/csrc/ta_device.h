@@ -78,61 +78,90 @@ __device__ __forceinline__ int load_bchunk(const int32_t* B, uint32_t m, uint32_
 // wave-lane k holds the dwords of stripes L0..L0+3 at step tt0+k (64 steps x
 // 64 rows).  Each iteration resolves a whole run of one op instead of one
 // cell (SURVEY §7 "traceback latency"):
-//   D (vertical)   -- the rows above in the same dword: counted on the SALU
-//                     (xor with the D pattern, count trailing zero fields);
+//   D (vertical)   -- the rows above in the same dword: the D plane shifted
+//                     so that row r is bit 0, counted on the SALU (trailing ones);
 //   I (horizontal) -- every wave-lane extracts row r of its step; the run is
 //                     the streak of I codes in the ballot going down from
 //                     the current step;
 //   M (diagonal)   -- every wave-lane extracts the diagonal cell of its step
 //                     (row r - (t - step)); same ballot streak.
-// Runs are clipped to the current stripe and tile; the next iteration picks
-// the walk up from there.  The CIGAR is written right to left into the slot.
-struct RleWriter {
-    char* end;       // one past the slot's last byte; bytes go to end[-1], end[-2], ...
+// The iteration computes the D run and the one ballot unconditionally and
+// picks with selects (no divergent control flow on the SALU).  Runs are
+// clipped to the current stripe and tile; the next iteration picks the walk
+// up from there.
+//
+// Runs are not formatted as they are found: RunWriter parks each finished
+// run (op, count) in lane nb of two VGPRs, and every 64 runs the wave formats
+// them at once -- each lane its own run's decimal digits, offsets from a
+// wave prefix sum -- right to left into the slot (the walk goes backwards).
+struct RunWriter {
+    char* end;       // one past the slot's last byte; text grows towards the front
     uint32_t used;   // bytes written so far
-    uint32_t op, cnt;
-    uint64_t total;
-    __device__ __forceinline__ void put(char c) {
-        ++used;
-        *(end - used) = c;  // every lane stores the same byte to the same address
-    }
-    __device__ __forceinline__ void flush() {
-        if (!cnt) return;
-        put((char)op);  // to_string(count) + op, written backwards
-        uint32_t c = cnt;
-        if (c < 10u) {
-            put((char)('0' + c));
-            return;
+    uint32_t op, cnt;  // the open run (op 0: nothing pushed yet)
+    uint32_t nb;     // runs parked in rc / ro
+    uint32_t rc, ro; // VGPRs: lane k = count / op char of parked run k
+    int lane;
+    __device__ __forceinline__ void flush_parked() {
+        const bool act = (uint32_t)lane < nb;
+        uint32_t c = rc;
+        const uint32_t digits = 1u + (c >= 10u) + (c >= 100u) + (c >= 1000u) + (c >= 10000u) + (c >= 100000u) +
+                                (c >= 1000000u) + (c >= 10000000u) + (c >= 100000000u) + (c >= 1000000000u);
+        const uint32_t L = act ? digits + 1u : 0u;
+        uint32_t incl = L;  // inclusive prefix sum over lanes
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t v = (uint32_t)__shfl_up((int)incl, o, 64);
+            if (lane >= o) incl += v;
         }
-        do {
-            const uint32_t q = c / 10u;
-            put((char)('0' + (c - 10u * q)));
-            c = q;
-        } while (c);
+        // run k's text ends where runs 0..k-1 (found earlier, written further right) begin
+        char* p = end - used - (incl - L) - 1;
+        if (act) *p = (char)ro;
+#pragma unroll
+        for (uint32_t d = 0; d < 10u; ++d) {  // fixed trip count: no divergent loop
+            if (d < digits && act) p[-1 - (int)d] = (char)('0' + c % 10u);
+            c /= 10u;
+        }
+        used += (uint32_t)rdlane((int)incl, 63);
+        nb = 0;
     }
+    __device__ __forceinline__ void park() {
+        const bool here = (uint32_t)lane == nb;
+        rc = here ? cnt : rc;
+        ro = here ? op : ro;
+        if (++nb == 64u) flush_parked();
+    }
+    // k >= 1 always (every caller moves the walk)
     __device__ __forceinline__ void push(uint32_t o, uint32_t k) {
-        total += k;
         if (o == op) {
             cnt += k;
-        } else {
-            flush();
-            op = o;
-            cnt = k;
+            return;
         }
+        if (op) park();
+        op = o;
+        cnt = k;
+    }
+    __device__ __forceinline__ void finish() {
+        if (!op) {  // RLE of an empty op string: "1" + '\0' (:145-160)
+            used = 2;
+            *(end - 2) = '1';
+            *(end - 1) = '\0';
+            return;
+        }
+        park();
+        if (nb) flush_parked();
     }
 };
 
-// length of the streak of set bits in b going down from bit `from` (>= 1 when bit `from` is set)
+// length of the streak of set bits in b going down from bit `from` (bit `from` is set)
 __device__ __forceinline__ uint32_t streak_down(uint64_t b, uint32_t from) {
-    const uint64_t y = ~(b << (63u - from));  // bit `from` -> 63; shifted-in zeros stop the streak
-    return y ? (uint32_t)__clzll((long long)y) : 64u;
+    return (uint32_t)__clzll((long long)~(b << (63u - from)));  // shifted-in zeros stop the streak
 }
 
 template <int MODE>
 __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, uint32_t m, uint32_t gi, uint32_t gj,
                                                char* slot, uint64_t cap, int lane, uint64_t* start_in_slot,
                                                uint32_t* len) {
-    RleWriter w{slot + cap, 0u, 0u, 0u, 0ull};
+    RunWriter w{slot + cap, 0u, 0u, 0u, 0u, 0u, 0u, lane};
     if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
         if (gi == n) {
             if (m - gj) w.push('I', m - gj);
@@ -144,12 +173,13 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
     uint32_t i = gi, j = gj;
     // tile = steps [tt0, tt0+64) x stripes [tL0, tL0+4) of pass tP.  The walk
     // never moves to a larger step or stripe within a pass, so only the lower
-    // bounds (and the pass) need checking.
-    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tL0 = 0;
-    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0;
+    // bounds (and the pass) need checking.  `cur` is the tile column of
+    // stripe cur_ln (re-selected only when the walk changes stripe).
+    uint32_t tP = 0xFFFFFFFFu, tt0 = 0, tL0 = 0, cur_ln = 0xFFFFFFFFu;
+    uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, cur = 0;
     while (true) {
         if (MODE == kLocal) {
-            if ((i == 0) | (j == 0)) break;  // row/col 0 cost 0 ends the walk (:202)
+            if (min(i, j) == 0) break;  // row/col 0 cost 0 ends the walk (:202)
         } else {
             if (i == 0) {  // row 0: INSERT parents (:89-92)
                 if (j) w.push('I', j);
@@ -161,60 +191,55 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
             }
         }
         const uint32_t row = i - 1;
-        const uint32_t pass = row >> 10;  // kPassRows = 1024
         const uint32_t ln = (row >> 4) & 63u, r = row & 15u;
         const uint32_t t = (j - 1) + ln;
-        if (((int)((t - tt0) | (ln - tL0)) < 0) | (pass != tP)) {
-            tP = pass;
-            tL0 = ln >= 3u ? ln - 3u : 0u;
-            tt0 = t >= 63u ? t - 63u : 0u;
+        if ((int)((t - tt0) | (ln - tL0)) < 0 || (row >> 10) != tP) {
+            // (readfirstlane: keeps the tile origin in SGPRs; hipcc computes
+            // the clamped subtractions on the VALU)
+            tP = row >> 10;  // kPassRows = 1024
+            tL0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(max(ln, 3u) - 3u));
+            tt0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(max(t, 63u) - 63u));
             const uint32_t ts = tt0 + (uint32_t)lane;
             c0 = c1 = c2 = c3 = 0;
             if (ts < Tmax) {
-                const uint32_t* q = P + ((uint64_t)pass * Tmax + ts) * kWave + tL0;
+                const uint32_t* q = P + ((uint64_t)tP * Tmax + ts) * kWave + tL0;
                 c0 = q[0];
                 c1 = q[1];
                 c2 = q[2];
                 c3 = q[3];
             }
+            cur_ln = 0xFFFFFFFFu;
         }
-        const uint32_t sel = ln - tL0;
-        const uint32_t comp = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
+        if (ln != cur_ln) {
+            const uint32_t sel = ln - tL0;
+            cur = sel == 0 ? c0 : sel == 1 ? c1 : sel == 2 ? c2 : c3;
+            cur_ln = ln;
+        }
         const uint32_t kk = t - tt0;
-        const uint32_t dw = (uint32_t)rdlane((int)comp, kk);
-        // bit planes (ta_internal.h Code): row r's D bit at 31 - r, I bit at 15 - r
+        // bit planes (ta_internal.h Code): row r's D bit at 31 - r, I bit at
+        // 15 - r.  x = dw >> (15 - r): bit 16 + k / bit k = D / I of row r - k.
         const uint32_t sh = 15u - r;
-        const uint32_t dbit = (dw >> (sh + kDPlane)) & 1u, ibit = (dw >> sh) & 1u;
-        if (MODE == kLocal && (dbit & ibit)) break;  // STOP: cost == 0 (:202)
-        uint32_t run;
-        if (dbit) {
-            // D cells of rows r, r-1, ..: the D plane (local: minus STOP cells)
-            // shifted so that row r is bit 0; the run is its trailing ones
-            uint32_t dp = dw >> kDPlane;
-            if (MODE == kLocal) dp &= ~dw;
-            run = (uint32_t)__builtin_ctz(~((dp & 0xFFFFu) >> sh));  // <= r + 1
-            w.push('D', run);
-            i -= run;
-        } else if (ibit) {
-            // row r at every step of the tile: I code = I bit set, D bit clear
-            const uint32_t v = (comp >> sh) & 0x10001u;
-            run = min(streak_down(ballot(v == 1u), kk), j);
-            w.push('I', run);
-            j -= run;
-        } else {
-            // diagonal: step tt0+lane holds row r - (kk - lane), i.e. shift sh + (kk - lane)
-            const uint32_t v = (comp >> ((sh + kk - (uint32_t)lane) & 31u)) & 0x10001u;
-            run = min(min(streak_down(ballot(v == 0u), kk), r + 1u), j);
-            w.push('M', run);
-            i -= run;
-            j -= run;
-        }
+        const uint32_t x = (uint32_t)rdlane((int)cur, kk) >> sh;
+        // Branch-free: the D run (SALU) and the one ballot (I: row r at every
+        // step; M: step tt0+lane holds row r - (kk - lane), i.e. shift
+        // sh + (kk - lane)) are both computed and picked with selects; hipcc
+        // turns uniform if/else chains here into costly flag-register flow.
+        const uint32_t dflag = (x >> 16) & 1u, iflag = x & 1u;
+        if (MODE == kLocal && (dflag & iflag)) break;  // STOP: cost == 0 (:202)
+        // D cells of rows r, r-1, .. (local: minus STOP cells): trailing ones
+        const uint32_t dp = (MODE == kLocal) ? ((x >> 16) & ~x) : (x >> 16);
+        const uint32_t drun = (uint32_t)__builtin_ctz(~dp);  // <= r + 1
+        const uint32_t lsh = sh + (kk - (uint32_t)lane) * (iflag ^ 1u);
+        const uint32_t v = (cur >> (lsh & 31u)) & 0x10001u;
+        const uint32_t streak = streak_down(ballot(v == iflag), kk);
+        const uint32_t hrun = min(streak, iflag ? j : min(j, r + 1u));
+        const uint32_t run = dflag ? drun : hrun;
+        const uint32_t op = dflag ? 'D' : ('M' - 4u * iflag);
+        w.push(op, run);
+        i -= (op == 'I') ? 0u : run;
+        j -= dflag ? 0u : run;
     }
-    w.flush();
-    if (w.total == 0) {  // RLE of an empty string: "1" + '\0' (:145-160)
-        w.put('\0');
-        w.put('1');
-    }
+    w.finish();
     *start_in_slot = cap - w.used;
     *len = w.used;
 }

@@ -76,6 +76,8 @@ __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
     return r;
 }
+// 0xFFFF in each half whose sign bit (15 / 31) is set
+__device__ __forceinline__ uint32_t half_mask(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x09090808u); }
 __device__ __forceinline__ uint32_t rep16(int v) { return ((uint32_t)v & 0xFFFFu) | ((uint32_t)v << 16); }
 __device__ __forceinline__ int lo16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 __device__ __forceinline__ int hi16(uint32_t x) { return (int)(int16_t)(x >> 16); }
@@ -123,12 +125,19 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     uint32_t recv = rep16(LOCAL ? -(int)ia : wmul(ia, init));
     uint32_t tc2 = 0;
     const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
-    // local clamp base Zb = zstep*j - (ia + 1) for this lane's column j (= t - lane + 1)
-    int zb = zstep * (0 - lane) - (int)(ia + 1);  // value at t = -1
-    uint32_t bestK = 0xFFFFFFFFu;  // per half: signed -1 = no cell yet
-    uint32_t bestj = 0;
-    int rowbest[2] = {INT_MIN, INT_MIN};
-    uint32_t rowbest_j[2] = {0, 0};
+    // Per-lane running values, both pairs packed, advanced once per step:
+    //   Zp = local clamp base Zb = zstep*j - (ia + 1) for this lane's column j
+    //   jj = j (= t - lane + 1);  maj = ma*j (semi: row n holds H = S + ma*j)
+    // (all at t = -1 here).  Running bests are updated branch-free: the sign
+    // of a saturating packed difference, spread over its half by v_perm,
+    // selects the new column with one v_bfi; the value is a packed max.
+    uint32_t Zp = rep16(zstep * (0 - lane) - (int)(ia + 1));
+    const uint32_t ZS2 = rep16(zstep);
+    uint32_t jj = rep16(-lane), maj = rep16(-ma * lane);
+    const uint32_t MA2 = rep16(ma);
+    // local: best key S - Zb = 16H - r (r = row in the stripe), -16 = no cell yet
+    uint32_t bestK = rep16(-16), bestj = 0;
+    uint32_t rowbest = rep16(-32768), rowbest_j = 0;  // semi: best of row n, its column
 
     uint32_t tcur[2], tnext[2];
 #pragma unroll
@@ -145,23 +154,27 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * Tmax * kWave : nullptr;
     uint32_t* prow1 = CIGAR ? io.ptrs[1] + (uint64_t)pass * Tmax * kWave : nullptr;
 
-    auto step = [&](uint32_t t, auto masked_tag) {
-        constexpr bool MASKED = decltype(masked_tag)::value;
-        if ((t & 255u) == 0 && t) {
+    // Chunk reloads (every 256 steps: target bytes; every 64: the boundary
+    // row of a later pass) are hoisted out of the step loop by run_steps.
+    auto reload = [&](uint32_t t) {
+        if ((t & 255u) == 0) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 tcur[h] = tnext[h];
                 tnext[h] = load_tchunk(io.T[h], m, (t >> 8) + 1, lane);
             }
         }
+        if (pass > 0) {
+            bcur = bnext;
+            bnext = load_bchunk(io.B, m, (t >> 6) + 1, lane);
+        }
+    };
+    auto step = [&](uint32_t t, auto masked_tag) {
+        constexpr bool MASKED = decltype(masked_tag)::value;
         uint32_t top;
         if (pass == 0) {
             top = rep16(LOCAL ? zstep * (int)(t + 1) : (init - ma) * (int)(t + 1));  // S(0, j)
         } else {
-            if ((t & 63u) == 0 && t) {
-                bcur = bnext;
-                bnext = load_bchunk(io.B, m, (t >> 6) + 1, lane);
-            }
             top = (uint32_t)rdlane(bcur, t & 63u);
         }
         const uint32_t sh = (t & 3u) * 8;
@@ -171,7 +184,9 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         const uint32_t prev = recv;
         recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
         tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
-        zb += zstep;
+        Zp = pk_add(Zp, ZS2);
+        jj = pk_add(jj, ONE);
+        if (MODE == kSemi) maj = pk_add(maj, MA2);
 
         const int j = (int)t - lane + 1;
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
@@ -187,7 +202,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             auto e_of = [&](int r) { return pk_min_u16(q2[r] ^ tc2, ONE); };  // 0 on a match, 1 otherwise
             uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
             uint32_t upv = recv;
-            uint32_t Z = rep16(zb);
+            uint32_t Z = Zp;
             static_for<0, R>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
                 const uint32_t old = H2[r];
@@ -222,38 +237,42 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                     const uint32_t full = pk_max(lo, tree_max<NV, R>(H2));
                     sk = ((uint32_t)lane == nl - 1) ? lo : full;
                 }
-                // key = S - Zbase + 15 = 16H + 15 - r (per half)
-                const uint32_t key = pk_add(pk_sub(sk, rep16(zb)), rep16(15));
-                const bool ua = lo16(key) > lo16(bestK), ub = hi16(key) > hi16(bestK);
-                const uint32_t keep = (ua ? 0u : 0xFFFFu) | (ub ? 0u : 0xFFFF0000u);
-                bestK = (bestK & keep) | (key & ~keep);
-                bestj = (bestj & keep) | (rep16(j) & ~keep);
+                // key = S - Zb = 16H - r per half; strict '>' keeps the first column (:186)
+                const uint32_t key = pk_sub(sk, Zp);
+                bestj = bfi(half_mask(pk_sub_sat(bestK, key)), jj, bestj);
+                bestK = pk_max(bestK, key);
             }
-            if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + ma*j
-                const uint32_t v = H2[NV - 1];
-                const int va = lo16(v) + ma * j, vb = hi16(v) + ma * j;
-                if (va > rowbest[0]) {
-                    rowbest[0] = va;
-                    rowbest_j[0] = (uint32_t)j;
-                }
-                if (vb > rowbest[1]) {
-                    rowbest[1] = vb;
-                    rowbest_j[1] = (uint32_t)j;
-                }
+            if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + ma*j, strict '>' (:271-278)
+                const uint32_t v = pk_add(H2[NV - 1], maj);
+                rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jj, rowbest_j);
+                rowbest = pk_max(rowbest, v);
             }
             if (has_next && (uint32_t)lane == nl - 1) io.B[j] = (int32_t)H2[R - 1];
         }
         if (CIGAR) {
             // per pair: [I rows 8-15, I rows 0-7, D rows 8-15, D rows 0-7] (ta_internal.h Code)
-            prow0[t * kWave + lane] = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
-            prow1[t * kWave + lane] = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
+            // 32-bit byte offset from the uniform row base (SGPR base + VGPR offset stores)
+            const uint32_t off = (t * kWave + (uint32_t)lane) * 4u;
+            *(uint32_t*)((char*)prow0 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
+            *(uint32_t*)((char*)prow1 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
         }
     };
     const uint32_t ramp_end = min(nl - 1, steps);
-    uint32_t t = 0;
-    for (; t < ramp_end; ++t) step(t, std::true_type{});
-    for (; t < m; ++t) step(t, std::false_type{});
-    for (; t < steps; ++t) step(t, std::true_type{});
+    const uint32_t every = (pass > 0) ? 64u : 256u;
+    uint32_t t = 0, next_reload = every;
+    auto run_steps = [&](uint32_t t_end, auto masked_tag) {
+        while (t < t_end) {
+            if (t == next_reload) {
+                reload(t);
+                next_reload += every;
+            }
+            const uint32_t blk = min(t_end, next_reload);
+            for (; t < blk; ++t) step(t, masked_tag);
+        }
+    };
+    run_steps(ramp_end, std::true_type{});
+    run_steps(m, std::false_type{});
+    run_steps(steps, std::true_type{});
 
     DualOut out;
 #pragma unroll
@@ -261,7 +280,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         PassOut& o = out.o[h];
         o = PassOut{INT_MIN, 0, 0, INT_MIN, 0, 0};
         if (LOCAL) {
-            const int K = h ? hi16(bestK) : lo16(bestK);
+            const int K = (h ? hi16(bestK) : lo16(bestK)) + 15;  // 16H + 15 - r, < 0: no cell
             const int v = ((uint32_t)lane >= nl || K < 0) ? -1 : (K >> 4);
             const int mx = wave_max(v);
             const int fl = first_lane(v == mx);
@@ -288,8 +307,8 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane((int)cr, fl) + 1;
             o.j = m;
             if (last_pass) {
-                o.row_h = rdlane(rowbest[h], nl - 1);
-                o.row_j = (uint32_t)rdlane((int)rowbest_j[h], nl - 1);
+                o.row_h = rdlane(h ? hi16(rowbest) : lo16(rowbest), nl - 1);  // -32768: never set
+                o.row_j = (uint32_t)rdlane((int)(h ? (rowbest_j >> 16) : (rowbest_j & 0xFFFFu)), nl - 1);
             }
         } else {
             if (last_pass) {
