@@ -30,13 +30,28 @@ def splitmix64_next(state: np.ndarray) -> np.ndarray:
         return z ^ (z >> np.uint64(31))
 
 
+def _mix(z: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * _M1
+        z = (z ^ (z >> np.uint64(27))) * _M2
+        return z ^ (z >> np.uint64(31))
+
+
+def stream(state0, k0: int, count: int) -> np.ndarray:
+    """Outputs ``k0 .. k0+count-1`` of the splitmix64 stream that starts from
+    ``state0`` (closed form: output k = mix(state0 + (k+1) * golden)).
+    ``state0`` may be an array (one stream per row)."""
+    st = np.asarray(state0, dtype=np.uint64)[..., None]
+    k = np.arange(k0 + 1, k0 + 1 + count, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        return _mix(st + k * _GOLDEN)
+
+
 def draws(seed: int, n_pairs: int, count: int, first_pair: int = 0) -> np.ndarray:
-    """``count`` splitmix64 outputs per pair -> uint64 array [n_pairs, count]."""
+    """``count`` splitmix64 outputs per pair -> uint64 array [n_pairs, count]
+    (pair p's stream starts from state ``seed ^ p``)."""
     st = np.uint64(seed) ^ np.arange(first_pair, first_pair + n_pairs, dtype=np.uint64)
-    out = np.empty((n_pairs, count), dtype=np.uint64)
-    for k in range(count):
-        out[:, k] = splitmix64_next(st)
-    return out
+    return stream(st, 0, count).reshape(n_pairs, count)
 
 
 @dataclass
@@ -148,3 +163,127 @@ def ragged_batch(n_pairs: int, min_len: int, max_len: int, seed: int = 0x5EED, a
     for p in range(n_pairs):
         pairs.append((sym[p, : ql[p]].tobytes(), sym[p, max_len : max_len + tl[p]].tobytes()))
     return from_pairs(pairs)
+
+
+# --- config 3 / 4 stand-in: a genome and ONT-like reads -----
+
+COMPLEMENT = np.arange(256, dtype=np.uint8)
+for _a, _b in (b"AT", b"TA", b"CG", b"GC"):
+    COMPLEMENT[_a] = _b
+
+
+def reverse_complement(seq: np.ndarray) -> np.ndarray:
+    """A<->T, C<->G, reversed; other bytes pass through (team_mapper.cpp:47-63)."""
+    return COMPLEMENT[seq[::-1]]
+
+
+def genome(length: int, seed: int = 0xEC011) -> np.ndarray:
+    """i.i.d. uniform ACGT genome (the E. coli K-12 stand-in is 4,641,652 bp)."""
+    out = np.empty(length, dtype=np.uint8)
+    step = 1 << 22
+    for k0 in range(0, length, step):
+        c = min(step, length - k0)
+        out[k0 : k0 + c] = ACGT[(stream(seed, k0, c) >> np.uint64(62)).astype(np.intp)]
+    return out
+
+
+@dataclass
+class ReadSet:
+    """Reads sampled from a genome: concatenated bytes + offsets/lengths, and
+    where each came from (forward-strand start, segment length, strand)."""
+
+    bytes: np.ndarray  # uint8
+    off: np.ndarray  # uint64 [R]
+    len: np.ndarray  # uint32 [R]
+    start: np.ndarray  # uint64 [R], forward coordinates
+    seg_len: np.ndarray  # uint32 [R]
+    rev: np.ndarray  # bool [R]
+
+    @property
+    def n_reads(self) -> int:
+        return int(self.len.shape[0])
+
+    def read(self, r: int) -> bytes:
+        o = int(self.off[r])
+        return self.bytes[o : o + int(self.len[r])].tobytes()
+
+
+def _mutate(seg: np.ndarray, d: np.ndarray, rate: float) -> np.ndarray:
+    ev = (d[0::2] >> np.uint64(11)).astype(np.float64) * (1.0 / 2**53)
+    eb = ACGT[(d[1::2] >> np.uint64(62)).astype(np.intp)]
+    r3 = rate / 3.0
+    sub = ev < r3
+    ins = (ev >= r3) & (ev < 2 * r3)
+    emit_base = ~((ev >= 2 * r3) & (ev < rate))
+    base = np.where(sub, eb, seg)
+    cnt = ins.astype(np.intp) + emit_base.astype(np.intp)
+    out = np.empty(int(cnt.sum()), dtype=np.uint8)
+    pos = np.cumsum(cnt) - cnt
+    out[pos[ins]] = eb[ins]
+    out[(pos + ins)[emit_base]] = base[emit_base]
+    return out
+
+
+def ont_reads(n_reads: int, ref: np.ndarray, seed: int = 0x0E7, median: float = 9000.0, sigma: float = 0.5,
+              min_len: int = 1000, max_len: int = 20000, error: float = 0.10, first_read: int = 0) -> ReadSet:
+    """ONT-like reads: log-normal segment lengths (median ``median``, clamped to
+    [min_len, max_len]), uniform start, 50 % reverse-complement strand, then
+    ``error`` total substitution/insertion/deletion rate (a third each).
+    Read r's stream starts from state ``seed ^ r``: 4 header draws (two for the
+    length, start, strand), then 2 draws per segment base."""
+    G = int(ref.shape[0])
+    max_len = min(max_len, G)
+    chunks, lens, starts, segs, revs = [], [], [], [], []
+    for r in range(first_read, first_read + n_reads):
+        st = np.uint64(seed) ^ np.uint64(r)
+        h = stream(st, 0, 4)
+        u1 = (float(h[0] >> np.uint64(11)) + 1.0) * (1.0 / 2**53)
+        u2 = float(h[1] >> np.uint64(11)) * (1.0 / 2**53)
+        z = np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+        L = int(min(max(round(median * np.exp(sigma * z)), min_len), max_len))
+        s = int(h[2] % np.uint64(G - L + 1))
+        rev = bool(h[3] >> np.uint64(63))
+        seg = ref[s : s + L]
+        if rev:
+            seg = reverse_complement(seg)
+        rd = _mutate(seg, stream(st, 4, 2 * L), error)
+        chunks.append(rd)
+        lens.append(rd.shape[0])
+        starts.append(s)
+        segs.append(L)
+        revs.append(rev)
+    ln = np.array(lens, dtype=np.uint32)
+    off = np.zeros(n_reads, dtype=np.uint64)
+    if n_reads:
+        off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+    b = np.concatenate(chunks) if chunks else np.zeros(0, np.uint8)
+    return ReadSet(b, off, ln, np.array(starts, dtype=np.uint64), np.array(segs, dtype=np.uint32),
+                   np.array(revs, dtype=bool))
+
+
+def origin_batch(reads: ReadSet, ref: np.ndarray) -> PairBatch:
+    """Config-3 stand-in pairs: each read against its true origin window, in
+    the read's orientation (a window of the reverse-complement reference for
+    reverse reads, as team_mapper.cpp:674-678 aligns them)."""
+    tgt = []
+    for r in range(reads.n_reads):
+        s, L = int(reads.start[r]), int(reads.seg_len[r])
+        seg = ref[s : s + L]
+        tgt.append(reverse_complement(seg) if reads.rev[r] else seg)
+    tl = reads.seg_len.copy()
+    toff = np.zeros(reads.n_reads, dtype=np.uint64)
+    if reads.n_reads:
+        toff[1:] = np.cumsum(tl[:-1], dtype=np.uint64)
+    tb = np.concatenate(tgt) if tgt else np.zeros(0, np.uint8)
+    return PairBatch(reads.bytes, reads.off.copy(), reads.len.copy(), tb, toff, tl)
+
+
+ECOLI_LEN = 4_641_652  # NC_000913.3
+
+
+def cfg3_batch(n_reads: int = 10000, first_read: int = 0, genome_seed: int = 0xEC011, read_seed: int = 0x0E7):
+    """Config 3 stand-in: reads of a 4.64 Mb i.i.d. genome against
+    their true-origin windows.  Returns (PairBatch, ReadSet, genome)."""
+    g = genome(ECOLI_LEN, genome_seed)
+    rs = ont_reads(n_reads, g, read_seed, first_read=first_read)
+    return origin_batch(rs, g), rs, g

@@ -286,3 +286,97 @@ int oracle_max_threads(void) {
     return 1;
 #endif
 }
+
+/*
+ * Size-independent property check (TEST INFRASTRUCTURE): walks a CIGAR the
+ * way team_alignment.cpp builds it and recomputes the score of that path, for
+ * batches too large to re-align on the CPU.  Returns 0 when the CIGAR
+ * consumes exactly what the mode requires and the path's score equals
+ * `score`; otherwise a nonzero code naming the first violated property.
+ *   global (cpp:123-160): path (0,0)->(n,m); every op is charged.
+ *   local  (cpp:201-237): path ends at the goal (gj = target_begin-1) and is
+ *                         charged in full; consumption <= n, m.
+ *   semi   (cpp:286-334): path (0,0)->(n,m); boundary runs (I on row 0, D on
+ *                         column 0) and the appended trailing run (I on row n,
+ *                         D on column m) are free.
+ */
+int oracle_cigar_check(const char* q, unsigned n, const char* t, unsigned m, int type, int match, int mismatch,
+                       int gap, const char* cig, size_t clen, int score, unsigned target_begin) {
+    /* parse runs */
+    size_t k = 0;
+    unsigned long nm = 0, ni = 0, nd = 0;
+    if (clen == 2 && cig[0] == '1' && cig[1] == '\0') /* empty op string (cpp:145-160) */
+        return (type == 1 ? score == 0 : (n == 0 && m == 0 && score == 0)) ? 0 : 1;
+    /* first pass: totals */
+    while (k < clen) {
+        unsigned long c = 0;
+        if (cig[k] < '0' || cig[k] > '9') return 2;
+        while (k < clen && cig[k] >= '0' && cig[k] <= '9') c = c * 10 + (unsigned long)(cig[k++] - '0');
+        if (k >= clen || c == 0) return 3;
+        char op = cig[k++];
+        if (op == 'M') nm += c;
+        else if (op == 'I') ni += c;
+        else if (op == 'D') nd += c;
+        else return 4;
+    }
+    unsigned long qi, tj;
+    if (type == 1) {
+        if (nm + nd > n || nm + ni > m || target_begin < 1 + nm + ni) return 5;
+        tj = target_begin - 1 - (nm + ni); /* path starts at column gj - (M+I), gj = target_begin - 1 */
+        qi = 0;                                /* row unknown: try every start row */
+    } else {
+        if (nm + nd != n || nm + ni != m) return 5;
+        qi = 0;
+        tj = 0;
+    }
+    unsigned long rows_hi = (type == 1) ? n - (nm + nd) : 0;
+    for (unsigned long r0 = 0; r0 <= rows_hi; ++r0) {
+        unsigned long i = (type == 1) ? r0 : qi, j = tj;
+        int s = 0, ok = 0;
+        size_t kk = 0;
+        while (kk < clen) {
+            unsigned long c = 0;
+            while (cig[kk] >= '0' && cig[kk] <= '9') c = c * 10 + (unsigned long)(cig[kk++] - '0');
+            const char op = cig[kk++];
+            const int last = kk >= clen;
+            /* semi: a trailing I run (row n) / D run (column m) may end in the
+             * appended free part (cpp:319-334), merged into the same RLE run:
+             * accept if the score matches after any genuine prefix of it */
+            const int tail = type == 2 && last && op != 'M';
+            if (tail && s == score) ok = 1;
+            for (unsigned long x = 0; x < c; ++x) {
+                int d;
+                if (op == 'M') {
+                    d = or_match(q[i], t[j], match, mismatch);
+                    ++i, ++j;
+                } else if (op == 'I') { /* row 0 = boundary: init per cell (cpp:83-92), never '-' */
+                    d = (i == 0) ? (type == 0 ? gap : 0) : or_indel(t[j], gap);
+                    ++j;
+                } else {
+                    d = (j == 0) ? (type == 0 ? gap : 0) : or_indel(q[i], gap);
+                    ++i;
+                }
+                s = wadd(s, d);
+                if (tail && s == score) ok = 1;
+            }
+        }
+        if (s == score) ok = 1;
+        if (ok) return 0;
+        if (type != 1) return type == 0 ? 6 : 7;
+    }
+    return 8;
+}
+
+int oracle_cigar_check_batch(unsigned n_pairs, const char* qbytes, const uint64_t* qoff, const uint32_t* qlen,
+                             const char* tbytes, const uint64_t* toff, const uint32_t* tlen, int type, int match,
+                             int mismatch, int gap, const int32_t* score, const uint32_t* target_begin,
+                             const char* arena, const uint64_t* cig_off, const uint32_t* cig_len, int32_t* status) {
+    long bad = 0;
+#pragma omp parallel for schedule(dynamic, 4) reduction(+ : bad)
+    for (long p = 0; p < (long)n_pairs; ++p) {
+        status[p] = oracle_cigar_check(qbytes + qoff[p], qlen[p], tbytes + toff[p], tlen[p], type, match, mismatch,
+                                       gap, arena + cig_off[p], cig_len[p], score[p], target_begin[p]);
+        bad += status[p] != 0;
+    }
+    return (int)bad;
+}

@@ -147,3 +147,23 @@ class BatchResult:
 
     def cigars(self):
         return [self.cigar(p) for p in range(len(self.scores))]
+
+
+def cigar_check_batch(batch, type, match, mismatch, gap, scores, target_begins, arena, cigar_off, cigar_len):
+    """Size-independent property check of a whole batch's results (see
+    oracle_cigar_check in align_oracle.c): per-pair status, 0 = consistent."""
+    build()
+    lib = C.CDLL(ORACLE_SO)
+    P = batch.n_pairs
+    st = np.zeros(P, np.int32)
+    sc = np.ascontiguousarray(scores, dtype=np.int32)
+    tb = np.ascontiguousarray(target_begins, dtype=np.uint32)
+    co = np.ascontiguousarray(cigar_off, dtype=np.uint64)
+    cl = np.ascontiguousarray(cigar_len, dtype=np.uint32)
+    ar = np.ascontiguousarray(arena, dtype=np.uint8)
+    lib.oracle_cigar_check_batch(
+        C.c_uint(P), _ptr(batch.qbytes, C.c_char), _ptr(batch.qoff, C.c_uint64), _ptr(batch.qlen, C.c_uint32),
+        _ptr(batch.tbytes, C.c_char), _ptr(batch.toff, C.c_uint64), _ptr(batch.tlen, C.c_uint32),
+        C.c_int(int(type)), C.c_int(match), C.c_int(mismatch), C.c_int(gap), _ptr(sc, C.c_int32),
+        _ptr(tb, C.c_uint32), _ptr(ar, C.c_char), _ptr(co, C.c_uint64), _ptr(cl, C.c_uint32), _ptr(st, C.c_int32))
+    return st

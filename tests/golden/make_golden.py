@@ -188,8 +188,13 @@ def make_digest(ref, name, batch, typ, m, n, g, desc):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-digests", action="store_true")
+    ap.add_argument("--only", default="", help="comma-separated digest names: regenerate only these")
     a = ap.parse_args()
     ref = Reference()
+    if a.only:
+        for name in a.only.split(","):
+            DIGEST_SPECS[name](ref)
+        return
     kat = kat_cases(ref)
     with open(os.path.join(OUT, "kat.json"), "w") as f:
         json.dump({"generated_by": "oracle/_ref (reference team_alignment.cpp)", "cases": kat}, f, indent=0)
@@ -217,6 +222,19 @@ def main():
                 "2000 ragged 0..3000 global, synth.ragged_batch(seed=0xF00D)")
     make_digest(ref, "cfg5_semi_sample", synth.related_batch(32, 10000, 10000, 0x5EED), 2, 1, -1, -1,
                 "config 5 linear-gap sample: 32 related 10kx10k semiGlobal, synth.related_batch(seed=0x5EED)")
+    for spec in DIGEST_SPECS.values():
+        spec(ref)
+
+
+def _cfg3_sample(ref):
+    b, _, _ = synth.cfg3_batch(64)
+    make_digest(ref, "cfg3_semi_sample", b, 2, 1, -1, -1,
+                "config 3 stand-in sample: first 64 ONT-like reads (1-20 kb, 10% error, 50% reverse) of "
+                "synth.cfg3_batch() vs their true-origin windows, semiGlobal 1/-1/-1")
+
+
+# digests added after the first set (regenerate one with --only NAME)
+DIGEST_SPECS = {"cfg3_semi_sample": _cfg3_sample}
 
 
 if __name__ == "__main__":

@@ -208,3 +208,37 @@ def test_team_align_dropin(kat_cases, random_cases):
         out = subprocess.run([exe] + mode, input="\n".join(lines) + "\n", capture_output=True, text=True,
                              timeout=600, check=True).stdout.splitlines()
         assert out == want
+
+
+def _check_full(aligner, batch, mode, sc):
+    from oracle.pyoracle import cigar_check_batch
+
+    r = aligner.align_batch(batch, mode, *sc, True)
+    st = cigar_check_batch(batch, mode, *sc, r.scores, r.target_begins, r.arena, r.cigar_offsets, r.cigar_lens)
+    assert not st.any(), (np.nonzero(st)[0][:8], st[np.nonzero(st)[0][:8]])
+    r0 = aligner.align_batch(batch, mode, *sc, False)
+    np.testing.assert_array_equal(r0.scores, r.scores)
+    np.testing.assert_array_equal(r0.target_begins, r.target_begins)
+    return r
+
+
+def test_config3_full_batch_properties(aligner):
+    """BASELINE config 3 stand-in at full size (10k ONT-like reads, 1-20 kb,
+    1.18e12 cells): every CIGAR is a full semi-global path whose score is the
+    reported score, and score-only mode agrees.  The first 64 pairs are
+    bit-exact against the reference digest (test_digest[cfg3_semi_sample])."""
+    b, _, _ = synth.cfg3_batch(10000)
+    r = _check_full(aligner, b, 2, (1, -1, -1))
+    meta, d = load_digest("cfg3_semi_sample")
+    np.testing.assert_array_equal(r.scores[:64], d["scores"])
+    np.testing.assert_array_equal(r.cigar_lens[:64], d["cigar_lens"])
+
+
+def test_config5_shape_properties(aligner):
+    """Config 5 shape (10 kb x 10 kb semi-global, linear gap) on 512 pairs:
+    path/score properties; the first 32 pairs bit-exact vs the reference digest."""
+    b = synth.related_batch(512, 10000, 10000, 0x5EED)
+    r = _check_full(aligner, b, 2, (1, -1, -1))
+    meta, d = load_digest("cfg5_semi_sample")
+    np.testing.assert_array_equal(r.scores[:32], d["scores"])
+    np.testing.assert_array_equal(r.cigar_lens[:32], d["cigar_lens"])

@@ -76,3 +76,28 @@ def test_oracle_matches_reference_fuzz(oracle):
         typ = int(rng.integers(0, 3))
         sm = schemes[k % len(schemes)]
         assert oracle.align(q, t, typ, *sm) == ref.align(q, t, typ, *sm), (q, t, typ, sm)
+
+
+def test_cigar_checker(oracle):
+    """The size-independent property checker (used on full-size GPU batches)
+    accepts every oracle result and rejects a corrupted score or CIGAR."""
+    from bioinfo1_amd import synth
+    from oracle.pyoracle import cigar_check_batch
+
+    batches = [synth.related_batch(40, 300, 280, seed=5), synth.ragged_batch(150, 0, 60, seed=3, alphabet=b"ACG-"),
+               synth.ragged_batch(100, 0, 40, seed=8, alphabet=b"acgtN")]
+    for mode in (0, 1, 2):
+        for b in batches:
+            for sc in ((1, -1, -1), (2, -3, -2), (2, -1, 2), (0, 0, 0), (1, 2, -3)):
+                r = oracle.align_batch(b, mode, *sc, True)
+                st = cigar_check_batch(b, mode, *sc, r.scores, r.target_begins, r.arena, r.offsets, r.cigar_lens)
+                assert not st.any(), (mode, sc, np.nonzero(st)[0][:5])
+        b = batches[0]
+        r = oracle.align_batch(b, mode, 1, -1, -1, True)
+        s = r.scores.copy()
+        s[3] += 1
+        assert cigar_check_batch(b, mode, 1, -1, -1, s, r.target_begins, r.arena, r.offsets, r.cigar_lens)[3] != 0
+        a = r.arena.copy()
+        o = int(r.offsets[5])
+        a[o] = ord("7") if a[o] != ord("7") else ord("6")  # wrong run length
+        assert cigar_check_batch(b, mode, 1, -1, -1, r.scores, r.target_begins, a, r.offsets, r.cigar_lens)[5] != 0
