@@ -22,7 +22,20 @@ done
 "$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$CS/ta_kernels.hip" -o "$B/ta_misc.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip" -o "$B/ta_api.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp" -o "$B/shim.o" & pids+=($!)
+# mapper stages (libteam_mapper.so) and the team_mapper_amd CLI
+for f in tm_minimizers tm_match tm_chain; do
+  "$HIPCC" "${FLAGS[@]}" -c "$CS/$f.hip" -o "$B/$f.o" & pids+=($!)
+done
+for f in tm_api tm_fastx; do
+  "$HIPCC" "${FLAGS[@]}" -x hip -c "$CS/$f.cpp" -o "$B/$f.o" & pids+=($!)
+done
+"$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp" -o "$B/tm_main.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_api.o" "$B/shim.o" -o "$OUT"
+PKG="$ROOT/bioinfo1_amd"
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/tm_{minimizers,match,chain,api,fastx}.o -L"$PKG" -lteam_alignment -lz \
+  -Wl,-rpath,'$ORIGIN' -o "$PKG/libteam_mapper.so"
+"$HIPCC" --offload-arch=gfx950 "$B/tm_main.o" -L"$PKG" -lteam_mapper -lteam_alignment -Wl,-rpath,'$ORIGIN' \
+  -o "$PKG/team_mapper_amd"
 make -s -C "$ROOT/oracle" >/dev/null
 echo "built $OUT"
