@@ -56,9 +56,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg5"],
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg5", "cfg3map"],
                     help="cfg2: 1kx1k pairs (headline); cfg3: E. coli stand-in, ONT-like reads vs true-origin "
-                         "windows, semiGlobal; cfg5: 10kx10k related semiGlobal (a sample of the 100k pairs)")
+                         "windows, semiGlobal; cfg5: 10kx10k related semiGlobal (a sample of the 100k pairs); "
+                         "cfg3map: config 3 end to end -- minimizer seeding, FindLIS chaining and semiGlobal "
+                         "alignment of the same reads against the 4.64 Mb genome (team_mapper pipeline)")
     ap.add_argument("--pairs", type=int, default=0, help="pairs per GPU (0 = the workload's default)")
     ap.add_argument("--qlen", type=int, default=1000)
     ap.add_argument("--tlen", type=int, default=1000)
@@ -69,15 +71,15 @@ def parse():
     ap.add_argument("--cpu-pairs", type=int, default=10000, help="CPU-baseline sample size (pairs)")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--workspace-gb", type=float, default=160.0,
-                    help="device budget for the 2-bit traceback codes (batches above it run in chunks)")
+    ap.add_argument("--workspace-gb", type=float, default=0.0,
+                    help="device budget (GB) for the 2-bit traceback codes; 0 = the library default (85%% of free HBM); batches above it run in chunks")
     ap.add_argument("--no-parity", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal only)")
     a = ap.parse_args()
     if a.workload == "cfg2":
         a.pairs = a.pairs or 10000
         a.mode = a.mode or "local"
-    elif a.workload == "cfg3":
+    elif a.workload in ("cfg3", "cfg3map"):
         a.pairs = a.pairs or 10000
         a.mode = a.mode or "semiGlobal"
         a.cpu_pairs = min(a.cpu_pairs, 200)
@@ -171,8 +173,143 @@ def load_traffic(tag):
     return t.get(tag)
 
 
+def write_fastx(path, recs, fastq):
+    with open(path, "wb") as f:
+        for name, seq in recs:
+            if fastq:
+                f.write(b"@" + name + b"\n" + seq + b"\n+\n" + b"I" * len(seq) + b"\n")
+            else:
+                f.write(b">" + name + b"\n" + seq + b"\n")
+
+
+def mapper_cpu_baseline_and_parity(genome, reads, sample, mode_name, tmpdir):
+    """oracle/_ref/ref_mapper (the reference's Minimize + Align, restated glue,
+    sequential) on the first `sample` reads, timed; and team_mapper_amd on the
+    same files, whose PAF lines must be byte-identical."""
+    import subprocess
+
+    from bioinfo1_amd import mapper as M
+    from oracle.pymapper import REF_MAPPER_BIN
+
+    os.makedirs(tmpdir, exist_ok=True)
+    gp, rp = os.path.join(tmpdir, "genome.fasta"), os.path.join(tmpdir, "reads.fastq")
+    write_fastx(gp, [(b"ecoli_syn", genome.tobytes())], False)
+    write_fastx(rp, [(b"read%d" % r, reads.read(r)) for r in range(sample)], True)
+    args = ["-a", mode_name, "-c", gp, rp]
+    res = {}
+    if os.path.exists(REF_MAPPER_BIN):
+        env = dict(os.environ, REF_MAPPER_TIMING="1")
+        t0 = time.perf_counter()
+        ref = subprocess.run([REF_MAPPER_BIN] + args, capture_output=True, env=env, check=True)
+        wall = time.perf_counter() - t0
+        tm = dict(kv.split("=") for kv in ref.stderr.decode().split("ref_mapper_timing ")[1].split())
+        cells = int(tm["aligned_cells"])
+        res["cpu_baseline"] = {"value": round(cells / float(tm["map_s"]) / 1e9, 4), "unit": "GCUPS", "cores": 1,
+                               "kind": "reference",
+                               "sample": f"first {sample} reads ({cells:.3g} aligned cells): reference Minimize + Align "
+                                         f"with the restated team_mapper glue, sequential; index build "
+                                         f"{float(tm['index_s']):.2f} s excluded, {wall:.1f} s wall",
+                               "impl": "oracle/_ref/ref_mapper"}
+        gpu = M.run_cli(args, timeout=300)
+        res["parity"] = {"golden": f"oracle/_ref/ref_mapper PAF on the first {sample} reads",
+                         "lines": ref.stdout.count(b"\n"), "bit_exact": gpu.returncode == 0 and gpu.stdout == ref.stdout}
+    return res
+
+
+def main_mapper(args):
+    """config 3 end to end: the team_mapper pipeline on the GPU (minimizers ->
+    seed hits -> FindLIS -> one alignment batch) for this rank's reads against
+    the whole 4.64 Mb genome (index replicated per GPU, reads range-split)."""
+    from bioinfo1_amd import mapper as M
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group(args.dist_backend)
+    dev_index = 0 if os.environ.get("TA_BENCH_ONE_GPU") == "1" else local_rank
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
+    mode = MODES[args.mode]
+    sc = tuple(int(x) for x in args.scoring.split(","))
+    g = synth.genome(synth.ECOLI_LEN)
+    rs = synth.ont_reads(args.pairs, g, first_read=rank * args.pairs)
+    reads = [rs.read(r) for r in range(rs.n_reads)]
+    mp = M.Mapper(dev_index)
+    t0 = time.perf_counter()
+    idx = M.Index(mp, "ecoli_syn", g.tobytes(), 15, 5, 0.001)
+    index_s = time.perf_counter() - t0
+    opt = M.Options.make(type=mode, match=sc[0], mismatch=sc[1], gap=sc[2], want_cigar=not args.no_cigar,
+                         fastq_rules=True)
+    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
+    rec = torch.zeros((2, args.pairs), dtype=torch.int32, device=coll_dev)
+    gathered = torch.zeros((world * 2, args.pairs), dtype=torch.int32, device=coll_dev) if world > 1 else None
+
+    def step():
+        r = idx.map_batch(reads, opt)
+        if world > 1:
+            rec[0].copy_(torch.from_numpy(r.scores))
+            rec[1].copy_(torch.from_numpy(r.mapped.astype(np.int32)))
+            dist.all_gather_into_tensor(gathered, rec)
+        return r
+
+    for _ in range(args.warmup):
+        step()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    stages = {}
+    for _ in range(args.steps):
+        r = step()
+        st, cells = mp.stage_times()
+        for k, v in st.items():
+            stages[k] = stages.get(k, 0.0) + v / args.steps
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    ms = elapsed / max(args.steps, 1) * 1e3
+    out = None
+    if rank == 0:
+        extra = {}
+        if world == 1 and not args.no_cpu:
+            extra = mapper_cpu_baseline_and_parity(g, rs, 24, args.mode, os.path.join(ROOT, "gpurun_out", "cfg3map"))
+        out = {
+            "metric": "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; bit-exact score+CIGAR",
+            "value": round(cells * world / (ms / 1e3) / 1e9, 2), "unit": "GCUPS", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
+            "config": {"workload": f"config 3 end to end: {args.pairs} ONT-like reads per GPU (log-normal 1-20 kb, "
+                                   f"10% error, 50% reverse, FASTQ rules) mapped to a 4.64 Mb synthetic genome: GPU "
+                                   f"minimizers, seed matching, FindLIS, {args.mode} alignment of the chained windows "
+                                   f"with CIGAR {'off' if args.no_cigar else 'on'}; host reads in, host results out",
+                       "reads_per_gpu": args.pairs, "mode": args.mode, "aligned_cells_per_gpu": cells,
+                       "parallelism": f"reads range-split over {world} GPU(s), index replicated, RCCL all-gather"},
+            "reads_mapped": int(r.mapped.sum()), "reads_per_s": round(args.pairs * world / (ms / 1e3), 1),
+            "index_build_s": round(index_s, 3), "stage_ms": {k: round(v, 3) for k, v in stages.items()},
+            "roofline": None, "device": torch.cuda.get_device_name(dev), **extra,
+        }
+    idx.close()
+    mp.close()
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+
+
 def main():
     args = parse()
+    if args.workload == "cfg3map":
+        return main_mapper(args)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))

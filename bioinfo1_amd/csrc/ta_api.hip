@@ -26,6 +26,10 @@ struct ta_context {
         size_t cap = 0;
     };
     Buf qbytes, tbytes, qoff, toff, score, tb, slots, cstart, clen, dst_off, dst;
+    // Traceback-code and pass-boundary workspace, shared by every plan of this
+    // context and grown at execute time (a plan's chunks are sized by its
+    // budget): plans of one context must not execute concurrently.
+    Buf ws_ptrs, ws_bnd;
 };
 
 struct ta_plan {
@@ -54,8 +58,6 @@ struct ta_plan {
     uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr, *d_singles = nullptr, *d_duals = nullptr;
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
     uint32_t *d_goal_i = nullptr, *d_goal_j = nullptr;
-    uint32_t* d_ptrs = nullptr;
-    int32_t* d_bnd = nullptr;
     uint32_t* d_fb = nullptr;  // dual fallback: [n_dual_pairs] list, then one counter per chunk
 };
 
@@ -75,9 +77,16 @@ int fail(ta_context* ctx, int code, const std::string& msg) {
 
 bool valid_type(int t) { return t == TA_GLOBAL || t == TA_LOCAL || t == TA_SEMI_GLOBAL; }
 
-uint64_t default_budget() {
+// Workspace budget when the caller passes 0: TA_WORKSPACE_BYTES, else 85 % of
+// what is free on the device (counting the context's cached workspace), so
+// long-read batches run in as few chunks as HBM allows (fewer, fuller
+// launches: one wave per pair needs thousands of pairs per chunk).
+uint64_t default_budget(const ta_context* ctx) {
     if (const char* e = std::getenv("TA_WORKSPACE_BYTES")) return std::strtoull(e, nullptr, 10);
-    return 48ull << 30;  // of the 288 GB HBM
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 48ull << 30;
+    const uint64_t avail = (uint64_t)free_b + ctx->ws_ptrs.cap + ctx->ws_bnd.cap;
+    return std::max<uint64_t>(avail / 100 * 85, 1ull << 30);
 }
 
 int grow(ta_context* ctx, ta_context::Buf& b, size_t bytes) {
@@ -141,7 +150,7 @@ void ta_context_destroy(ta_context* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     for (auto* b : {&ctx->qbytes, &ctx->tbytes, &ctx->qoff, &ctx->toff, &ctx->score, &ctx->tb, &ctx->slots,
-                    &ctx->cstart, &ctx->clen, &ctx->dst_off, &ctx->dst})
+                    &ctx->cstart, &ctx->clen, &ctx->dst_off, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd})
         if (b->p) (void)hipFree(b->p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -152,7 +161,7 @@ void ta_plan_destroy(ta_plan* pl) {
     (void)hipSetDevice(pl->ctx->device);
     for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_ptr_off,
                     (void*)pl->d_bnd_off, (void*)pl->d_slot_off, (void*)pl->d_goal_i, (void*)pl->d_goal_j,
-                    (void*)pl->d_ptrs, (void*)pl->d_bnd, (void*)pl->d_fb})
+                    (void*)pl->d_fb})
         if (p) (void)hipFree(p);
     delete pl;
 }
@@ -191,7 +200,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
         if (ca != cb) return ca > cb;
         return pl->qlen[a] != pl->qlen[b] ? pl->qlen[a] > pl->qlen[b] : pl->tlen[a] > pl->tlen[b];
     });
-    if (budget == 0) budget = default_budget();
+    if (budget == 0) budget = default_budget(ctx);
     const uint64_t budget_dw = std::max<uint64_t>(budget / 4, 1);
     std::vector<uint64_t> ptr_off(n_pairs, 0), bnd_off(n_pairs, 0);
     pl->slot_off.assign(n_pairs, 0);
@@ -259,11 +268,6 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
             hipMalloc(&pl->d_goal_j, n_pairs * 4ull) != hipSuccess)
             rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc goal");
     }
-    if (rc == TA_OK && pl->ws_ptr_dwords &&
-        hipMalloc(&pl->d_ptrs, pl->ws_ptr_dwords * 4ull) != hipSuccess)
-        rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc pointer workspace");
-    if (rc == TA_OK && pl->ws_bnd_words && hipMalloc(&pl->d_bnd, pl->ws_bnd_words * 4ull) != hipSuccess)
-        rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc boundary workspace");
     if (rc == TA_OK && pl->n_dual_pairs &&
         hipMalloc(&pl->d_fb, (pl->n_dual_pairs + pl->chunks.size()) * 4ull) != hipSuccess)
         rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc dual fallback list");
@@ -284,6 +288,13 @@ uint32_t ta_plan_dual_pairs(const ta_plan* pl) { return pl ? pl->n_dual_pairs : 
 
 static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill, bool trace) {
     const auto& ch = pl->chunks[c];
+    ta_context* ctx = pl->ctx;
+    if (pl->ws_ptr_dwords)
+        if (int r = grow(ctx, ctx->ws_ptrs, pl->ws_ptr_dwords * 4ull)) return r;
+    if (pl->ws_bnd_words)
+        if (int r = grow(ctx, ctx->ws_bnd, pl->ws_bnd_words * 4ull)) return r;
+    uint32_t* d_ptrs = static_cast<uint32_t*>(ctx->ws_ptrs.p);
+    int32_t* d_bnd = static_cast<int32_t*>(ctx->ws_bnd.p);
     if (fill) {
         ta::FillArgs a{};
         a.order = pl->d_order;
@@ -298,9 +309,9 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         a.match = pl->match;
         a.mismatch = pl->mismatch;
         a.gap = pl->gap;
-        a.ptrs = pl->d_ptrs;
+        a.ptrs = d_ptrs;
         a.ptr_off = pl->d_ptr_off;
-        a.bnd = pl->d_bnd;
+        a.bnd = d_bnd;
         a.bnd_off = pl->d_bnd_off;
         a.score = io->score;
         a.target_begin = io->target_begin;
@@ -343,7 +354,7 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         t.count = ch.count;
         t.qlen = pl->d_qlen;
         t.tlen = pl->d_tlen;
-        t.ptrs = pl->d_ptrs;
+        t.ptrs = d_ptrs;
         t.ptr_off = pl->d_ptr_off;
         t.goal_i = pl->d_goal_i;
         t.goal_j = pl->d_goal_j;

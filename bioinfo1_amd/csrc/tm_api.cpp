@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -129,7 +130,7 @@ void tm_context_destroy(tm_context* c) {
     for (tmap::DevBuf* b : {&c->bytes, &c->off, &c->len, &m.entry_off, &m.tiles, &m.hash, &m.pos, &m.keep, &m.scan,
                           &m.kept_off, &m.khash, &m.kpos, &m.cub_tmp, &c->c_off, &c->c_f, &c->c_r, &c->c_out,
                           &c->c_prev, &c->c_lis, &c->m_qoff, &c->m_toff, &c->m_score, &c->m_tb, &c->m_slots,
-                          &c->m_cstart, &c->m_clen, &c->match.cnt_f, &c->match.cnt_r, &c->match.off_f,
+                          &c->m_cstart, &c->m_clen, &c->m_coff, &c->m_cdst, &c->match.cnt_f, &c->match.cnt_r, &c->match.off_f,
                           &c->match.off_r, &c->match.key_f, &c->match.key_r, &c->match.hf, &c->match.hr,
                           &c->match.list_off, &c->match.cub_tmp})
         b->release();
@@ -239,17 +240,32 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
     TM_HIP(ctx, ctx->bytes.reserve(nbytes + 1));
     TM_HIP(ctx, ctx->off.reserve(n_reads * 8ull));
     TM_HIP(ctx, ctx->len.reserve(n_reads * 4ull));
+    using clk = std::chrono::steady_clock;
+    auto t_last = clk::now();
+    const auto t_first = t_last;
+    std::fill(ctx->stage_ms, ctx->stage_ms + tmap::kStages, 0.0);
+    auto stage = [&](int i) -> int {  // close stage i (the stream is drained so host time = device time)
+        TM_HIP(ctx, hipStreamSynchronize(s));
+        const auto t = clk::now();
+        ctx->stage_ms[i] = std::chrono::duration<double, std::milli>(t - t_last).count();
+        ctx->stage_ms[tmap::kStages - 1] = std::chrono::duration<double, std::milli>(t - t_first).count();
+        t_last = t;
+        return TM_OK;
+    };
     if (nbytes) TM_HIP(ctx, hipMemcpyAsync(ctx->bytes.p, bytes, nbytes, hipMemcpyHostToDevice, s));
     TM_HIP(ctx, hipMemcpyAsync(ctx->off.p, off, n_reads * 8ull, hipMemcpyHostToDevice, s));
     TM_HIP(ctx, hipMemcpyAsync(ctx->len.p, len, n_reads * 4ull, hipMemcpyHostToDevice, s));
+    if (int r = stage(0)) return r;
     // 1. read minimizers, first occurrences only (team_mapper.cpp:611-612, 713-714)
     tmap::MinimizerOut& mo = ctx->mins;
     if (int r = tmap::minimize_device(ctx, n_reads, ctx->bytes.as<uint8_t>(), ctx->off.as<uint64_t>(),
                                     ctx->len.as<uint32_t>(), len, opt->k, opt->w, true, mo))
         return r;
+    if (int r = stage(1)) return r;
     // 2. seed hits on both strands
     tmap::MatchOut& mt = ctx->match;
     if (int r = tmap::match_device(ctx, n_reads, mo, idx->fwd.view(), idx->rev.view(), opt->fastq_rules, mt)) return r;
+    if (int r = stage(2)) return r;
     // 3. FindLIS per (read, strand)
     const uint32_t n_lists = 2 * n_reads;
     TM_HIP(ctx, ctx->c_out.reserve(n_lists * 20ull));
@@ -259,6 +275,7 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
     std::vector<uint32_t> ch(5ull * n_lists);
     TM_HIP(ctx, hipMemcpyAsync(ch.data(), ctx->c_out.p, n_lists * 20ull, hipMemcpyDeviceToHost, s));
     TM_HIP(ctx, hipStreamSynchronize(s));
+    if (int r = stage(3)) return r;
     // 4. windows (team_mapper.cpp:650-663)
     const uint32_t k = opt->k;
     std::vector<uint32_t> pair_read, ql, tl;
@@ -315,39 +332,49 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
         io.cigar_slots = ctx->m_slots.as<char>();
         io.cigar_start = ctx->m_cstart.as<uint64_t>();
         io.cigar_len = ctx->m_clen.as<uint32_t>();
+        if (int r = stage(4)) return r;
         if (int r = ta_plan_execute(plan, &io, s))
             return fail(ctx, TM_ERR_DEVICE, std::string("ta_plan_execute: ") + ta_last_error(ctx->ta) + " (" +
                                                 ta_status_string(r) + ")");
+        if (int r = stage(5)) return r;
         std::vector<int32_t> sc(P);
         TM_HIP(ctx, hipMemcpyAsync(sc.data(), ctx->m_score.p, P * 4ull, hipMemcpyDeviceToHost, s));
-        std::vector<uint64_t> cs;
-        std::vector<uint32_t> cl;
-        std::vector<char> sl;
+        std::vector<uint64_t> co;
+        uint64_t total = 0;
         if (opt->want_cigar) {
-            cs.resize(P);
-            cl.resize(P);
-            sl.resize(slots);
-            TM_HIP(ctx, hipMemcpyAsync(cs.data(), ctx->m_cstart.p, P * 8ull, hipMemcpyDeviceToHost, s));
-            TM_HIP(ctx, hipMemcpyAsync(cl.data(), ctx->m_clen.p, P * 4ull, hipMemcpyDeviceToHost, s));
-            if (slots) TM_HIP(ctx, hipMemcpyAsync(sl.data(), ctx->m_slots.p, slots, hipMemcpyDeviceToHost, s));
+            // pack the CIGAR slots on the device, then copy only the CIGAR bytes
+            if (int r = tmap::compact_segments(ctx, P, ctx->m_slots.as<const char>(), ctx->m_cstart.as<const uint64_t>(),
+                                               ctx->m_clen.as<const uint32_t>(), ctx->m_coff, ctx->m_cdst,
+                                               ctx->match.cub_tmp, total))
+                return r;
+            if (total > arena_bytes) return fail(ctx, TM_ERR_CAPACITY, "cigar arena too small");
+            co.resize(P + 1);
+            TM_HIP(ctx, hipMemcpyAsync(co.data(), ctx->m_coff.p, (P + 1) * 8ull, hipMemcpyDeviceToHost, s));
+            if (total) TM_HIP(ctx, hipMemcpyAsync(arena, ctx->m_cdst.p, total, hipMemcpyDeviceToHost, s));
         }
         TM_HIP(ctx, hipStreamSynchronize(s));
-        uint64_t o = 0;
         for (uint32_t p = 0; p < P; ++p) {
             const uint32_t r = pair_read[p];
             score[r] = sc[p];
             if (!opt->want_cigar) continue;
-            if (o + cl[p] > arena_bytes) return fail(ctx, TM_ERR_CAPACITY, "cigar arena too small");
-            std::memcpy(arena + o, sl.data() + cs[p], cl[p]);
-            cigar_off[r] = o;
-            cigar_len[r] = cl[p];
-            o += cl[p];
+            cigar_off[r] = co[p];
+            cigar_len[r] = (uint32_t)(co[p + 1] - co[p]);
         }
         return TM_OK;
     };
     rc = run();
     ta_plan_destroy(plan);
+    if (rc == TM_OK) rc = stage(6);
+    ctx->stage_cells = 0;
+    for (uint32_t p = 0; p < P; ++p) ctx->stage_cells += (uint64_t)ql[p] * tl[p];
     return rc;
+}
+
+int tm_stage_times(const tm_context* ctx, double* ms, uint32_t n, uint64_t* aligned_cells) {
+    if (!ctx || (n && !ms)) return TM_ERR_ARG;
+    for (uint32_t i = 0; i < n && i < (uint32_t)tmap::kStages; ++i) ms[i] = ctx->stage_ms[i];
+    if (aligned_cells) *aligned_cells = ctx->stage_cells;
+    return TM_OK;
 }
 
 int tm_map_files(const char* reference_path, const char* reads_path, const tm_options* opt, const char* out_path,

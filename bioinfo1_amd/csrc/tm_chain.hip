@@ -13,8 +13,9 @@
 // list's order: over the prefix where f is non-decreasing (all hits of the
 // leading and full-window minimizers) every eligible j lies in the window
 // f_j > f_i - 5000, tracked by a moving lower bound; hits after that prefix
-// (trailing end-minimizers) scan all earlier j.  Lists up to kCap hits live
+// (trailing end-minimizers) scan all earlier j.  Lists up to kCapBig hits live
 // in LDS (f, r, lis, prev); longer lists run the same code on global scratch.
+// (kCapSmall / kCapBig: two LDS sizes, see chain_kernel.)
 // The wave that owns i-1's result keeps it in registers, so iteration i needs
 // no second barrier before reading lis[i-1].
 #include <hip/hip_runtime.h>
@@ -29,7 +30,8 @@ namespace tmap {
 namespace {
 
 constexpr int kChainBlock = 256;
-constexpr int kCap = 3072;  // hits per list staged in LDS (36 KB)
+constexpr int kCapSmall = 3072;  // hits per list staged in LDS: 36 KB, 4 workgroups per CU
+constexpr int kCapBig = 12288;   // 144 KB, 1 workgroup per CU (gfx950: up to 160 KB per workgroup)
 
 template <class FT, class LT>
 __device__ __forceinline__ void lis_list(int n, const FT* F, const FT* R, LT* LIS, LT* PREV, uint64_t* red, int* sorted_end,
@@ -114,20 +116,27 @@ __device__ __forceinline__ void lis_list(int n, const FT* F, const FT* R, LT* LI
     }
 }
 
-__global__ __launch_bounds__(kChainBlock) void chain_kernel(uint32_t n_lists, const uint64_t* __restrict__ off,
+// Lists with lo < n <= CAP run in LDS; with CAP == kCapBig the kernel also
+// takes every longer list (global scratch).  Two instantiations: a small-LDS
+// one (4 workgroups per CU) for the common lists and a large-LDS one for the
+// long reads' lists.
+template <int CAP>
+__global__ __launch_bounds__(kChainBlock) void chain_kernel(uint32_t n_lists, int lo_excl,
+                                                            const uint64_t* __restrict__ off,
                                                             const uint32_t* __restrict__ f,
                                                             const uint32_t* __restrict__ r,
                                                             uint32_t* __restrict__ g_lis, uint32_t* __restrict__ g_prev,
                                                             uint32_t* __restrict__ out) {
-    __shared__ uint32_t sF[kCap], sR[kCap];
-    __shared__ uint16_t sL[kCap], sP[kCap];
+    __shared__ uint32_t sF[CAP], sR[CAP];
+    __shared__ uint16_t sL[CAP], sP[CAP];
     __shared__ uint64_t red[8];
     __shared__ int sorted_end;
     const uint32_t l = blockIdx.x;
     if (l >= n_lists) return;
     const uint64_t b = off[l];
     const int n = (int)(off[l + 1] - b);
-    if (n <= kCap) {
+    if (n <= lo_excl || (CAP != kCapBig && n > CAP)) return;  // another instantiation's list
+    if (n <= CAP) {
         for (int j = threadIdx.x; j < n; j += kChainBlock) {
             sF[j] = f[b + j];
             sR[j] = r[b + j];
@@ -146,8 +155,11 @@ int chain_device(tm_context* ctx, uint32_t n_lists, const uint64_t* d_off, uint6
     if (!n_lists) return TM_OK;
     TM_HIP(ctx, ctx->c_lis.reserve(total_hits * 4 + 4));
     TM_HIP(ctx, ctx->c_prev.reserve(total_hits * 4 + 4));
-    chain_kernel<<<n_lists, kChainBlock, 0, ctx->stream>>>(n_lists, d_off, d_f, d_r, ctx->c_lis.as<uint32_t>(),
-                                                           ctx->c_prev.as<uint32_t>(), d_out);
+    chain_kernel<kCapSmall><<<n_lists, kChainBlock, 0, ctx->stream>>>(
+        n_lists, -1, d_off, d_f, d_r, ctx->c_lis.as<uint32_t>(), ctx->c_prev.as<uint32_t>(), d_out);
+    TM_HIP(ctx, hipGetLastError());
+    chain_kernel<kCapBig><<<n_lists, kChainBlock, 0, ctx->stream>>>(
+        n_lists, kCapSmall, d_off, d_f, d_r, ctx->c_lis.as<uint32_t>(), ctx->c_prev.as<uint32_t>(), d_out);
     TM_HIP(ctx, hipGetLastError());
     return TM_OK;
 }

@@ -18,6 +18,7 @@ constexpr uint32_t kMaxK = 15;
 constexpr uint32_t kMaxW = 64;
 constexpr int kMinTile = 1024;  // minimizer entries per workgroup
 constexpr int kMinBlock = 256;
+constexpr int kStages = 8;  // tm_stage_times: upload, minimizers, matching, chaining, windows+plan, align, results, total
 
 // Entries KMER::Minimize emits for a sequence of length L
 // (team_minimizers.cpp:146-222): w-1 leading end-minimizers (the reference
@@ -89,7 +90,9 @@ struct tm_context {
     tmap::MatchOut match;
     tmap::DevBuf c_off, c_f, c_r, c_out, c_prev, c_lis;
     // tm_map_batch
-    tmap::DevBuf m_qoff, m_toff, m_score, m_tb, m_slots, m_cstart, m_clen;
+    tmap::DevBuf m_qoff, m_toff, m_score, m_tb, m_slots, m_cstart, m_clen, m_coff, m_cdst;
+    double stage_ms[tmap::kStages] = {};
+    uint64_t stage_cells = 0;
 };
 
 namespace tmap {

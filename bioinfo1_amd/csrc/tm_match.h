@@ -10,4 +10,9 @@ hipError_t launch_revcomp(const uint8_t* in, uint8_t* out, uint64_t L, hipStream
 int match_device(tm_context* ctx, uint32_t n_reads, const MinimizerOut& m, const DevIndexView& fi,
                  const DevIndexView& ri, int fastq_rules, MatchOut& out);
 
+// Packs n byte segments src[start[p] .. + len[p]) back to back into dst;
+// d_off[0..n] = their offsets (inclusive scan shifted), total = bytes.
+int compact_segments(tm_context* ctx, uint32_t n, const char* d_src, const uint64_t* d_start, const uint32_t* d_len,
+                     DevBuf& d_off, DevBuf& d_dst, DevBuf& tmp, uint64_t& total);
+
 }  // namespace tmap

@@ -86,7 +86,45 @@ __global__ void revcomp_kernel(const uint8_t* __restrict__ in, uint8_t* __restri
     out[i] = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'G' ? 'C' : c == 'C' ? 'G' : c;
 }
 
+__global__ void widen_kernel(uint32_t n, const uint32_t* __restrict__ in, uint64_t* __restrict__ out) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = in[i];
+}
+
+// one workgroup per segment: bytes src[start[p] .. + len[p]) -> dst[off[p] ..)
+__global__ void gather_segments_kernel(const char* __restrict__ src, const uint64_t* __restrict__ start,
+                                       const uint32_t* __restrict__ len, const uint64_t* __restrict__ off,
+                                       char* __restrict__ dst) {
+    const uint32_t p = blockIdx.x;
+    const char* a = src + start[p];
+    char* b = dst + off[p];
+    for (uint32_t i = threadIdx.x; i < len[p]; i += blockDim.x) b[i] = a[i];
+}
+
 }  // namespace
+
+int compact_segments(tm_context* ctx, uint32_t n, const char* d_src, const uint64_t* d_start, const uint32_t* d_len,
+                     DevBuf& d_off, DevBuf& d_dst, DevBuf& tmp, uint64_t& total) {
+    hipStream_t s = ctx->stream;
+    total = 0;
+    if (!n) return TM_OK;
+    TM_HIP(ctx, d_off.reserve((n + 1) * 8ull));
+    size_t tb = 0;
+    TM_HIP(ctx, hipcub::DeviceScan::InclusiveSum(nullptr, tb, d_off.as<uint64_t>(), d_off.as<uint64_t>() + 1, (int)n, s));
+    const size_t tb_al = (tb + 255) & ~(size_t)255;
+    TM_HIP(ctx, tmp.reserve(tb_al + n * 8ull));
+    uint64_t* len64 = reinterpret_cast<uint64_t*>(tmp.as<char>() + tb_al);  // scan input, apart from its output
+    widen_kernel<<<(n + 255) / 256, 256, 0, s>>>(n, d_len, len64);
+    TM_HIP(ctx, hipGetLastError());
+    TM_HIP(ctx, hipcub::DeviceScan::InclusiveSum(tmp.p, tb, len64, d_off.as<uint64_t>() + 1, (int)n, s));
+    TM_HIP(ctx, hipMemsetAsync(d_off.p, 0, 8, s));
+    TM_HIP(ctx, hipMemcpyAsync(&total, d_off.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, s));
+    TM_HIP(ctx, hipStreamSynchronize(s));
+    TM_HIP(ctx, d_dst.reserve(total + 1));
+    gather_segments_kernel<<<n, 256, 0, s>>>(d_src, d_start, d_len, d_off.as<uint64_t>(), d_dst.as<char>());
+    TM_HIP(ctx, hipGetLastError());
+    return TM_OK;
+}
 
 hipError_t launch_revcomp(const uint8_t* in, uint8_t* out, uint64_t L, hipStream_t s) {
     if (!L) return hipSuccess;

@@ -31,7 +31,7 @@ TM_OK = 0
 # Every symbol include/team_mapper_c.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = ["tm_status_string", "tm_last_error", "tm_context_create", "tm_context_destroy", "tm_minimizer_bound",
                "tm_minimize_batch", "tm_chain_batch", "tm_index_create", "tm_index_destroy", "tm_index_stats",
-               "tm_map_batch", "tm_map_files"]
+               "tm_map_batch", "tm_stage_times", "tm_map_files"]
 
 _lib = None
 
@@ -75,6 +75,7 @@ def lib() -> C.CDLL:
     L.tm_index_stats.argtypes = [vp, u64p, u64p, u64p, u64p, u32p, u32p]
     L.tm_map_batch.argtypes = [vp, vp, C.c_uint32, vp, u64p, u32p, C.POINTER(Options), u8p, u8p, u32p, u32p, u32p,
                                u32p, i32p, vp, C.c_uint64, u64p, u32p]
+    L.tm_stage_times.argtypes = [vp, C.POINTER(C.c_double), C.c_uint32, u64p]
     L.tm_map_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Options), C.c_char_p, C.c_int]
     _lib = L
     return L
@@ -136,6 +137,15 @@ class Mapper:
                                    int(dedup), _p(oo, C.c_uint64), _p(h, C.c_uint32), _p(p, C.c_uint32), cap),
                self._h)
         return [(h[int(oo[s]):int(oo[s + 1])].copy(), p[int(oo[s]):int(oo[s + 1])].copy()) for s in range(len(ln))]
+
+    STAGES = ["upload", "minimizers", "matching", "chaining", "windows_plan", "align", "results", "total"]
+
+    def stage_times(self):
+        """Per-stage wall ms of the last map_batch on this context, and its aligned cells."""
+        ms = (C.c_double * 8)()
+        cells = C.c_uint64()
+        _check(lib().tm_stage_times(self._h, ms, 8, C.byref(cells)))
+        return dict(zip(self.STAGES, list(ms))), cells.value
 
     # -- chaining -----------------------------------------------------------
     def chain_batch(self, lists):

@@ -115,6 +115,13 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
                  uint32_t* q_end, uint32_t* t_begin, uint32_t* t_end, int32_t* score, char* cigar_arena,
                  uint64_t cigar_arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len);
 
+/* Wall time (ms) of the last tm_map_batch on this context, per stage:
+ * [0] read upload, [1] minimizers, [2] seed matching, [3] FindLIS chaining,
+ * [4] windows + alignment plan (host), [5] alignment (fill + traceback),
+ * [6] results to host, [7] total; and the DP cells the alignment batch
+ * covered.  Stages are separated by stream synchronisations. */
+int tm_stage_times(const tm_context* ctx, double* ms, uint32_t n, uint64_t* aligned_cells);
+
 /*
  * The whole mapper on files (the reference's main, team_mapper.cpp:319-796):
  * reference FASTA (first record) and reads (FASTQ, else FASTA; plain or

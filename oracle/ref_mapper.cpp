@@ -30,6 +30,7 @@
  *  - main() (with -DREF_MAPPER_MAIN): the restated mapper CLI, PAF on stdout.
  */
 #include <algorithm>
+#include <chrono>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -233,6 +234,7 @@ int main(int argc, char** argv) {
     }
     if (file1.empty() || file2.empty()) return 1;
 
+    const auto t0 = std::chrono::steady_clock::now();
     // reference + its reverse complement, minimizers and frequencies (:398-430)
     std::vector<Rec> refs = read_fasta(file1);
     const Rec& R = refs.front();
@@ -274,6 +276,8 @@ int main(int argc, char** argv) {
         }
     }
 
+    const auto t1 = std::chrono::steady_clock::now();
+    uint64_t cells = 0, mapped = 0;
     for (const Rec& rd : reads) {  // :596-698 (FASTA), :709-789 (FASTQ)
         team::KMER kq(true);
         if (!fastq) kq.SetFrequenciesCount(false);
@@ -309,6 +313,8 @@ int main(int argc, char** argv) {
             std::cerr << "ERROR: Exception during Align: " << e.what() << std::endl;
             continue;
         }
+        cells += (uint64_t)(qe - qb + 1) * (te - tb + 1);
+        ++mapped;
         // PAF-like line (:686-697): reverse hits are reported in forward coordinates
         std::cout << rd.name << "\t" << rd.seq.size() << "\t" << qb << "\t" << (qe + 1) << "\t" << (fwd ? "+" : "-")
                   << "\t" << R.name << "\t" << ref.size() << "\t"
@@ -317,6 +323,12 @@ int main(int argc, char** argv) {
                   << "\t60";
         if (want_cigar) std::cout << "\tcg:Z:" << cigar;
         std::cout << std::endl;
+    }
+    if (std::getenv("REF_MAPPER_TIMING")) {
+        const auto t2 = std::chrono::steady_clock::now();
+        std::cerr << "ref_mapper_timing index_s=" << std::chrono::duration<double>(t1 - t0).count()
+                  << " map_s=" << std::chrono::duration<double>(t2 - t1).count() << " reads=" << reads.size()
+                  << " mapped=" << mapped << " aligned_cells=" << cells << std::endl;
     }
     return 0;
 }

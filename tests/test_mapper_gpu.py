@@ -92,10 +92,10 @@ def test_chain_vs_findlis(mp):
 
 
 def test_chain_long_lists_global_path(mp):
-    # > 3072 hits: the kernel's global-memory path
+    # 3072 < n <= 12288: the large-LDS instantiation; > 12288: global scratch
     rng = random.Random(5)
-    lists = []
-    for n in (3073, 5000):
+    lists = [[(i + 1, i + 1) for i in range(3072)]]
+    for n in (3073, 5000, 12289):
         f = sorted(rng.randint(1, 40000) for _ in range(n))
         lists.append([(x, x + rng.randint(-30, 30) + 1000) for x in f])
     got = mp.chain_batch(lists)
