@@ -245,15 +245,16 @@ def main_mapper(args):
     opt = M.Options.make(type=mode, match=sc[0], mismatch=sc[1], gap=sc[2], want_cigar=not args.no_cigar,
                          fastq_rules=True)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-    rec = torch.zeros((2, args.pairs), dtype=torch.int32, device=coll_dev)
-    gathered = torch.zeros((world * 2, args.pairs), dtype=torch.int32, device=coll_dev) if world > 1 else None
 
     def step():
         r = idx.map_batch(reads, opt)
-        if world > 1:
-            rec[0].copy_(torch.from_numpy(r.scores))
-            rec[1].copy_(torch.from_numpy(r.mapped.astype(np.int32)))
-            dist.all_gather_into_tensor(gathered, rec)
+        if world > 1:  # config 4: gather every rank's records and CIGAR bytes in read order (RCCL over xGMI)
+            from bioinfo1_amd import shard
+
+            n_cig = int(r.cigar_len.sum()) if opt.want_cigar else 0
+            cig = torch.from_numpy(r.arena[:n_cig]).to(coll_dev) if opt.want_cigar else None
+            t = lambda a: torch.from_numpy(a.view(np.int32)).to(coll_dev)  # noqa: E731
+            shard.gather_results(dist, t(r.scores), t(r.t_begin), t(r.cigar_len), cig, device=coll_dev)
         return r
 
     for _ in range(args.warmup):
@@ -292,7 +293,8 @@ def main_mapper(args):
                                    f"minimizers, seed matching, FindLIS, {args.mode} alignment of the chained windows "
                                    f"with CIGAR {'off' if args.no_cigar else 'on'}; host reads in, host results out",
                        "reads_per_gpu": args.pairs, "mode": args.mode, "aligned_cells_per_gpu": cells,
-                       "parallelism": f"reads range-split over {world} GPU(s), index replicated, RCCL all-gather"},
+                       "parallelism": f"reads range-split over {world} GPU(s), index replicated, RCCL all-gather "
+                                      f"of per-read records and CIGAR bytes (config 4 when world = 8)"},
             "reads_mapped": int(r.mapped.sum()), "reads_per_s": round(args.pairs * world / (ms / 1e3), 1),
             "index_build_s": round(index_s, 3), "stage_ms": {k: round(v, 3) for k, v in stages.items()},
             "roofline": None, "device": torch.cuda.get_device_name(dev), **extra,
