@@ -82,6 +82,8 @@ def lib() -> C.CDLL:
     L.ta_plan_chunks.argtypes = [C.c_void_p]
     L.ta_plan_dual_pairs.restype = C.c_uint32
     L.ta_plan_dual_pairs.argtypes = [C.c_void_p]
+    L.ta_plan_flex_pairs.restype = C.c_uint32
+    L.ta_plan_flex_pairs.argtypes = [C.c_void_p]
     L.ta_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ta_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     L.ta_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
@@ -93,7 +95,7 @@ def lib() -> C.CDLL:
 ABI_SYMBOLS = [
     "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_cigar_slot_bytes",
     "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes",
-    "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_execute", "ta_plan_execute_fill", "ta_plan_execute_traceback",
+    "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_execute", "ta_plan_execute_fill", "ta_plan_execute_traceback",
 ]
 # The drop-in C++ entry point (team_alignment.hpp), g++/libstdc++ cxx11 mangling.
 TEAM_ALIGN_SYMBOL = ("_ZN4team5AlignEPKcjS1_jNS_13AlignmentTypeEiiiPNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEEPj")
@@ -258,6 +260,7 @@ class DevicePlan:
         self.workspace_bytes = int(L.ta_plan_workspace_bytes(h))
         self.chunks = int(L.ta_plan_chunks(h))
         self.dual_pairs = int(L.ta_plan_dual_pairs(h))
+        self.flex_pairs = int(L.ta_plan_flex_pairs(h))
 
     def _stream(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)

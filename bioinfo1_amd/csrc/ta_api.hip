@@ -18,6 +18,10 @@
 struct ta_context {
     int device = 0;
     hipStream_t stream = nullptr;
+    // a second stream on which a chunk's int32 fill (single pairs) runs beside
+    // its packed two-pair fill; the caller's stream waits for it (fork / join)
+    hipStream_t aux = nullptr, aux2 = nullptr;  // aux2: the equal-shape dual fill beside the flexible one
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
     std::string last_error;
     std::mutex mu;  // one batch at a time per context
     // grow-only device staging for ta_align_batch
@@ -43,19 +47,23 @@ struct ta_plan {
     // traceback kernel walks every pair on its own wave (measured faster).
     bool fused = true;
     bool dual = true;   // packed two-pair int16 fill where it fits (TA_DUAL=0 disables)
-    std::vector<uint32_t> qlen, tlen, order, singles, duals;
+    bool flex = true;   // ... also for couples of different shapes / long pairs (TA_FLEX=0 disables)
+    std::vector<uint32_t> qlen, tlen, order, singles, duals, flexes;
     std::vector<uint64_t> slot_off;
     struct Chunk {
         uint32_t begin, count;    // all pairs (traceback order)
         uint32_t sbegin, scount;  // int32 fill: pairs
         uint32_t dbegin, dcount;  // dual fill: pair couples
+        uint32_t fbegin, fcount;  // flexible dual fill: pair couples
+        uint32_t cbegin;          // couples (dual + flex) before this chunk: its slice of the fallback list
         uint64_t ptr_dwords, bnd_words;
     };
     uint32_t n_dual_pairs = 0;
     std::vector<Chunk> chunks;
     uint64_t slots_bytes = 0, ws_ptr_dwords = 0, ws_bnd_words = 0;
     // device
-    uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr, *d_singles = nullptr, *d_duals = nullptr;
+    uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr, *d_singles = nullptr, *d_duals = nullptr,
+             *d_flexes = nullptr;
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
     uint32_t *d_goal_i = nullptr, *d_goal_j = nullptr;
     uint32_t* d_fb = nullptr;  // dual fallback: [n_dual_pairs] list, then one counter per chunk
@@ -138,7 +146,12 @@ int ta_context_create(int device, ta_context** out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TA_ERR_DEVICE;  // kernels are gfx950-only
     auto* c = new ta_context();
     c->device = device;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return TA_ERR_DEVICE;
     }
@@ -153,13 +166,18 @@ void ta_context_destroy(ta_context* ctx) {
                     &ctx->cstart, &ctx->clen, &ctx->dst_off, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd})
         if (b->p) (void)hipFree(b->p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
+    if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
+    if (ctx->ev_join2) (void)hipEventDestroy(ctx->ev_join2);
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
     delete ctx;
 }
 
 void ta_plan_destroy(ta_plan* pl) {
     if (!pl) return;
     (void)hipSetDevice(pl->ctx->device);
-    for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_ptr_off,
+    for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_flexes, (void*)pl->d_ptr_off,
                     (void*)pl->d_bnd_off, (void*)pl->d_slot_off, (void*)pl->d_goal_i, (void*)pl->d_goal_j,
                     (void*)pl->d_fb})
         if (p) (void)hipFree(p);
@@ -210,40 +228,110 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
         so += ta::cigar_slot_bytes(pl->qlen[p], pl->tlen[p]);
     }
     pl->slots_bytes = so;
-    ta_plan::Chunk cur{0, 0, 0, 0, 0, 0, 0, 0};
-    auto open_chunk = [&](uint32_t k) {
-        cur = ta_plan::Chunk{k, 0, (uint32_t)pl->singles.size(), 0, (uint32_t)(pl->duals.size() / 2), 0, 0, 0};
+    if (const char* e = std::getenv("TA_FLEX")) pl->flex = std::atoi(e) != 0;
+    // Work units: one pair (int32 fill), an equal-shape couple (dual fill) or
+    // a couple of different shapes (flexible dual fill), then longest first.
+    struct Unit {
+        int kind;  // 0 single, 1 dual, 2 flex
+        uint32_t a, b;
+        uint64_t cost;  // cells one wave sweeps
     };
-    open_chunk(0);
+    std::vector<Unit> units;
+    std::vector<uint32_t> rest;
     for (uint32_t k = 0; k < n_pairs;) {
         const uint32_t p = pl->order[k];
         const uint32_t n = pl->qlen[p], m = pl->tlen[p];
         const bool couple = pl->dual && k + 1 < n_pairs && pl->qlen[pl->order[k + 1]] == n &&
                             pl->tlen[pl->order[k + 1]] == m && ta::fits_int16(type, n, m, match, mismatch, gap);
-        const uint32_t units = couple ? 2 : 1;
-        const uint64_t pd = pl->want_cigar ? units * ta::ptr_dwords(n, m) : 0;
+        if (couple) {
+            units.push_back({1, p, pl->order[k + 1], (uint64_t)n * m});
+            k += 2;
+        } else {
+            rest.push_back(p);
+            ++k;
+        }
+    }
+    if (pl->dual && pl->flex && ta::flex_fits(type, match, mismatch, gap)) {
+        // flexible couples: same pass count and n mod 16 (same rows in the last
+        // lane), neighbours by (n, m), at most 25 % of the wave's cells wasted
+        std::vector<uint32_t> cand;
+        for (uint32_t p : rest) {
+            if (pl->qlen[p] && pl->tlen[p]) cand.push_back(p);
+            else units.push_back({0, p, p, (uint64_t)pl->qlen[p] * pl->tlen[p]});
+        }
+        auto key = [&](uint32_t p) { return ((uint64_t)ta::n_passes(pl->qlen[p]) << 4) | (pl->qlen[p] & 15u); };
+        std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) {
+            if (key(a) != key(b)) return key(a) < key(b);
+            if (pl->qlen[a] != pl->qlen[b]) return pl->qlen[a] > pl->qlen[b];
+            return pl->tlen[a] > pl->tlen[b];
+        });
+        for (size_t i = 0; i < cand.size();) {
+            const uint32_t A = cand[i];
+            if (i + 1 < cand.size() && key(cand[i + 1]) == key(A)) {
+                const uint32_t B = cand[i + 1];
+                const uint64_t M = std::max(pl->tlen[A], pl->tlen[B]);
+                const uint64_t wave = (uint64_t)pl->qlen[A] * M;
+                const uint64_t useful = (uint64_t)pl->qlen[A] * pl->tlen[A] + (uint64_t)pl->qlen[B] * pl->tlen[B];
+                if (4 * useful >= 3 * 2 * wave) {  // waste <= 25 %
+                    units.push_back({2, A, B, wave});
+                    i += 2;
+                    continue;
+                }
+            }
+            units.push_back({0, A, A, (uint64_t)pl->qlen[A] * pl->tlen[A]});
+            ++i;
+        }
+    } else {
+        for (uint32_t p : rest) units.push_back({0, p, p, (uint64_t)pl->qlen[p] * pl->tlen[p]});
+    }
+    std::stable_sort(units.begin(), units.end(), [](const Unit& x, const Unit& y) { return x.cost > y.cost; });
+    pl->order.clear();
+    ta_plan::Chunk cur{};
+    uint32_t couples_before = 0;
+    auto open_chunk = [&]() {
+        cur = ta_plan::Chunk{(uint32_t)pl->order.size(), 0, (uint32_t)pl->singles.size(), 0,
+                             (uint32_t)(pl->duals.size() / 2), 0, (uint32_t)(pl->flexes.size() / 2), 0,
+                             couples_before, 0, 0};
+    };
+    open_chunk();
+    for (const Unit& u : units) {
+        const uint32_t na = pl->qlen[u.a], ma = pl->tlen[u.a], nb = pl->qlen[u.b], mb = pl->tlen[u.b];
+        const uint64_t pd = !pl->want_cigar ? 0 : ta::ptr_dwords(na, ma) + (u.kind ? ta::ptr_dwords(nb, mb) : 0);
         if (cur.count && cur.ptr_dwords + pd > budget_dw) {
             pl->chunks.push_back(cur);
-            open_chunk(k);
+            open_chunk();
         }
-        for (uint32_t u = 0; u < units; ++u) {
-            const uint32_t q = pl->order[k + u];
-            ptr_off[q] = cur.ptr_dwords;
-            bnd_off[q] = cur.bnd_words;
-            cur.ptr_dwords += pl->want_cigar ? ta::ptr_dwords(n, m) : 0;
-            cur.bnd_words += ta::bnd_words(n, m);
+        const uint32_t q[2] = {u.a, u.b};
+        for (int h = 0; h < (u.kind ? 2 : 1); ++h) {
+            const uint32_t x = q[h];
+            ptr_off[x] = cur.ptr_dwords;
+            bnd_off[x] = cur.bnd_words;
+            cur.ptr_dwords += pl->want_cigar ? ta::ptr_dwords(pl->qlen[x], pl->tlen[x]) : 0;
+            // flex: pair A holds both pairs' absolute int32 boundary rows, interleaved;
+            // each pair keeps a region of its own for the int32 fallback ('-' in a query)
+            uint64_t bw = ta::bnd_words(pl->qlen[x], pl->tlen[x]);
+            if (u.kind == 2 && h == 0 && ta::n_passes(na) > 1)
+                bw = std::max<uint64_t>(bw, 2ull * ((uint64_t)std::max(ma, mb) + 1 + ta::kWave));
+            cur.bnd_words += bw;
+            pl->order.push_back(x);
         }
-        if (couple) {
-            pl->duals.push_back(p);
-            pl->duals.push_back(pl->order[k + 1]);
+        if (u.kind == 1) {
+            pl->duals.push_back(u.a);
+            pl->duals.push_back(u.b);
             ++cur.dcount;
-            pl->n_dual_pairs += 2;
+        } else if (u.kind == 2) {
+            pl->flexes.push_back(u.a);
+            pl->flexes.push_back(u.b);
+            ++cur.fcount;
         } else {
-            pl->singles.push_back(p);
+            pl->singles.push_back(u.a);
             ++cur.scount;
         }
-        cur.count += units;
-        k += units;
+        if (u.kind) {
+            pl->n_dual_pairs += 2;
+            ++couples_before;
+        }
+        cur.count += u.kind ? 2 : 1;
     }
     if (cur.count) pl->chunks.push_back(cur);
     if (pl->n_dual_pairs) pl->fused = false;
@@ -260,6 +348,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     up(upload(ctx, &pl->d_order, pl->order));
     up(upload(ctx, &pl->d_singles, pl->singles));
     up(upload(ctx, &pl->d_duals, pl->duals));
+    up(upload(ctx, &pl->d_flexes, pl->flexes));
     up(upload(ctx, &pl->d_ptr_off, ptr_off));
     up(upload(ctx, &pl->d_bnd_off, bnd_off));
     up(upload(ctx, &pl->d_slot_off, pl->slot_off));
@@ -285,6 +374,7 @@ uint64_t ta_plan_workspace_bytes(const ta_plan* pl) {
 }
 uint32_t ta_plan_chunks(const ta_plan* pl) { return pl ? (uint32_t)pl->chunks.size() : 0; }
 uint32_t ta_plan_dual_pairs(const ta_plan* pl) { return pl ? pl->n_dual_pairs : 0; }
+uint32_t ta_plan_flex_pairs(const ta_plan* pl) { return pl ? (uint32_t)pl->flexes.size() : 0; }
 
 static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill, bool trace) {
     const auto& ch = pl->chunks[c];
@@ -322,29 +412,61 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         a.slot_off = pl->d_slot_off;
         a.cigar_start = io->cigar_start;
         a.cigar_len = io->cigar_len;
-        if (ch.dcount) {
-            ta::FillArgs d = a;
-            d.order = pl->d_duals;
-            d.begin = ch.dbegin;
-            d.count = ch.dcount;
-            d.fb_list = pl->d_fb + 2ull * ch.dbegin;
-            d.fb_count = pl->d_fb + pl->n_dual_pairs + c;
-            TA_HIP(pl->ctx, hipMemsetAsync(d.fb_count, 0, 4, s));
-            TA_HIP(pl->ctx, ta::launch_dual(pl->type, pl->want_cigar, d, s));
-            // couples the dual kernel handed back ('-' in a query): int32 fill,
-            // wave count read on the device (grid sized for all of them)
+        if (ch.scount) {  // launched first: it may run on the aux stream beside the packed fill
+            ta::FillArgs a1 = a;
+            a1.order = pl->d_singles;
+            a1.begin = ch.sbegin;
+            a1.count = ch.scount;
+            if (ch.dcount || ch.fcount) {  // beside the packed fill: fork onto the aux stream, join below
+                TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
+                TA_HIP(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
+                TA_HIP(ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, a1, ctx->aux));
+            } else {
+                TA_HIP(ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, a1, s));
+            }
+        }
+        if (ch.dcount || ch.fcount) {
+            uint32_t* fb_list = pl->d_fb + 2ull * ch.cbegin;
+            uint32_t* fb_count = pl->d_fb + pl->n_dual_pairs + c;
+            TA_HIP(pl->ctx, hipMemsetAsync(fb_count, 0, 4, s));
+            if (ch.dcount) {
+                ta::FillArgs d = a;
+                d.order = pl->d_duals;
+                d.begin = ch.dbegin;
+                d.count = ch.dcount;
+                d.fb_list = fb_list;
+                d.fb_count = fb_count;
+                if (ch.fcount) {  // beside the flexible fill: fork onto aux2 (after the counter reset), join below
+                    TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
+                    TA_HIP(ctx, hipStreamWaitEvent(ctx->aux2, ctx->ev_fork, 0));
+                    TA_HIP(ctx, ta::launch_dual(pl->type, pl->want_cigar, d, ctx->aux2));
+                    TA_HIP(ctx, hipEventRecord(ctx->ev_join2, ctx->aux2));
+                } else {
+                    TA_HIP(ctx, ta::launch_dual(pl->type, pl->want_cigar, d, s));
+                }
+            }
+            if (ch.fcount) {
+                ta::FillArgs d = a;
+                d.order = pl->d_flexes;
+                d.begin = ch.fbegin;
+                d.count = ch.fcount;
+                d.fb_list = fb_list;
+                d.fb_count = fb_count;
+                TA_HIP(pl->ctx, ta::launch_flex(pl->type, pl->want_cigar, d, s));
+            }
+            if (ch.dcount && ch.fcount) TA_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_join2, 0));
+            // couples the packed kernels handed back ('-' in a query): int32
+            // fill, wave count read on the device (grid sized for all of them)
             ta::FillArgs f = a;
-            f.order = d.fb_list;
+            f.order = fb_list;
             f.begin = 0;
-            f.count = 2 * ch.dcount;
-            f.count_dev = d.fb_count;
+            f.count = 2 * (ch.dcount + ch.fcount);
+            f.count_dev = fb_count;
             TA_HIP(pl->ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, f, s));
         }
-        if (ch.scount) {
-            a.order = pl->d_singles;
-            a.begin = ch.sbegin;
-            a.count = ch.scount;
-            TA_HIP(pl->ctx, ta::launch_fill(pl->type, pl->want_cigar, pl->wide, a, s));
+        if (ch.scount && (ch.dcount || ch.fcount)) {  // join the aux stream
+            TA_HIP(ctx, hipEventRecord(ctx->ev_join, ctx->aux));
+            TA_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_join, 0));
         }
     }
     if (trace && pl->want_cigar && !(fill && pl->fused)) {

@@ -1,0 +1,370 @@
+// bioinfo1_amd/csrc/ta_flex.hip -- the packed two-pair fill for pairs of
+// DIFFERENT shapes and any length (global / semi-global), so ragged long-read
+// batches (config 3: 1-20 kb windows) get the v_pk_* throughput of
+// ta_dual.hip.  Same results and the same 2-bit pointer codes as the int32
+// fill; the traceback kernel is shared.
+//
+// What differs from dual_pass (ta_dual.hip):
+//  * Wave-uniform rebasing.  The stored value is V = S - O with S = H - ma*j
+//    and O a per-pair wave-uniform int32 offset.  Every 64 steps all lanes
+//    subtract the same packed value from all their cells (O absorbs it), so
+//    values exchanged between lanes need no conversion.  In a linear-gap DP
+//    adjacent cells differ by at most max|score| + |gap|, so
+//    the ~1,024 x 64 cells a wave holds, plus 64 steps of drift, span a few
+//    thousand: V fits int16 for any n and m, where absolute S does not
+//    (S reaches -(n+m) on a 20 kb pair).  Everything absolute -- the pass
+//    boundary row, the best of row n, the column-m candidates, the corner --
+//    is kept in int32 as V + O.
+//  * Two shapes.  The couple shares the query pass count and n mod 16 (so the
+//    last lane of the last pass holds the same NV rows for both), pair A has
+//    the larger n, and the wave runs max(mA, mB) columns.  Pair B's cells
+//    past its own n or m never feed its valid cells (the recurrence only
+//    looks up and left), so they are computed and ignored: its pointer codes
+//    are stored only for its own steps, its column-m candidates and corner
+//    are captured when the lanes reach column mB, its row-n best only counts
+//    columns <= mB and is read from its own last lane.
+#include "ta_device.h"
+#include "ta_packed.h"
+
+namespace ta {
+namespace {
+
+#ifdef TA_FLEX_MODE
+
+__device__ __forceinline__ int sext_lo(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
+__device__ __forceinline__ int sext_hi(uint32_t x) { return (int)(int16_t)(x >> 16); }
+
+struct FlexIo {
+    const uint8_t* Q[2];
+    const uint8_t* T[2];
+    uint32_t* ptrs[2];
+    int32_t* B;  // boundary row: absolute S per column and pair, [2*j + h]
+    uint32_t n[2], m[2];
+};
+
+struct FlexOut {
+    PassOut o[2];
+};
+
+// 64 columns per chunk of the absolute boundary row, pair h
+__device__ __forceinline__ int load_bchunk2(const int32_t* B, uint32_t M, uint32_t k, int lane, int h) {
+    const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+    return j <= M ? B[2 * j + h] : 0;
+}
+
+template <int MODE, bool CIGAR, int NV>
+__device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io, uint32_t pass, bool last_pass,
+                                             bool tdash, int lane) {
+    constexpr int R = kRows;
+    const int ma = a.match, mi = a.mismatch, gap = a.gap;
+    const int init = (MODE == kGlobal) ? gap : 0;
+    const uint32_t KD = rep16(mi - ma);
+    const int glg = gap - ma;  // left gain, target byte != '-'
+    const int gld = -ma;       // left gain, target byte == '-'
+    const uint32_t GUG = rep16(gap);
+    uint32_t ONE = 0x00010001u;
+    asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16
+    const uint32_t M = max(io.m[0], io.m[1]);
+    const uint32_t n = io.n[0];  // pair A has the larger n
+    const uint32_t row_base = pass * kPassRows;
+    const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
+    const uint32_t nl = (nrows + R - 1) / R;
+    const uint32_t nlh[2] = {nl, (min((uint32_t)kPassRows, io.n[1] - row_base) + R - 1) / R};
+    const bool has_next = !last_pass;
+
+    // offsets: S(i, 0) = i * init, so start from the pass's first row
+    int O[2] = {wmul(row_base, init), wmul(row_base, init)};
+    uint32_t q2[R], H2[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i0 = row_base + (uint32_t)lane * R + r;
+        q2[r] = (i0 < io.n[0] ? (uint32_t)io.Q[0][i0] : 0u) | ((i0 < io.n[1] ? (uint32_t)io.Q[1][i0] : 0u) << 16);
+        H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init));  // S(i, 0) - O
+    }
+    uint32_t recv = rep16(wmul((uint32_t)lane * R, init));
+    uint32_t tc2 = 0;
+    // captures (absolute int32): column m_h candidates (semi) / corner (global), row-n best (semi)
+    int capv[2] = {INT_MIN, INT_MIN}, capr[2] = {0, 0};
+    int rb[2] = {INT_MIN, INT_MIN};
+    uint32_t rbj[2] = {0, 0};
+
+    uint32_t tcur[2], tnext[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        tcur[h] = load_tchunk(io.T[h], io.m[h], 0, lane);
+        tnext[h] = load_tchunk(io.T[h], io.m[h], 1, lane);
+    }
+    int bcur[2] = {0, 0}, bnext[2] = {0, 0};
+    if (pass > 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            bcur[h] = load_bchunk2(io.B, M, 0, lane, h);
+            bnext[h] = load_bchunk2(io.B, M, 1, lane, h);
+        }
+    }
+    const uint32_t steps = M + nl - 1;
+    const uint32_t Tmax0 = pass_steps(io.m[0]), Tmax1 = pass_steps(io.m[1]);
+    uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * Tmax0 * kWave : nullptr;
+    uint32_t* prow1 = CIGAR ? io.ptrs[1] + (uint64_t)pass * Tmax1 * kWave : nullptr;
+
+    auto reload = [&](uint32_t t) {
+        if ((t & 255u) == 0) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                tcur[h] = tnext[h];
+                tnext[h] = load_tchunk(io.T[h], io.m[h], (t >> 8) + 1, lane);
+            }
+        }
+        if (pass > 0) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                bcur[h] = bnext[h];
+                bnext[h] = load_bchunk2(io.B, M, (t >> 6) + 1, lane, h);
+            }
+        }
+        // rebase (every 64 steps, all lanes alike): a lane that holds current cells
+        const uint32_t d = (uint32_t)rdlane((int)H2[0], t < M ? 0u : nl - 1);
+#pragma unroll
+        for (int r = 0; r < R; ++r) H2[r] = pk_sub(H2[r], d);
+        recv = pk_sub(recv, d);
+        O[0] += sext_lo(d);
+        O[1] += sext_hi(d);
+    };
+    auto capture = [&](int h, int j, bool active) {
+        // lanes at column m_h: this pass's column-m candidates (semi) or the corner (global)
+        if (!active || j != (int)io.m[h]) return;
+        const int oh = O[h];
+        if (MODE == kSemi) {
+            const uint32_t nv = (uint32_t)lane < nlh[h] - 1 ? R : ((uint32_t)lane == nlh[h] - 1 ? NV : 0);
+            int cv = INT_MIN, cr = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int v = (h ? sext_hi(H2[r]) : sext_lo(H2[r])) + oh;
+                if ((uint32_t)r < nv && v > cv) {
+                    cv = v;
+                    cr = r;
+                }
+            }
+            capv[h] = cv;
+            capr[h] = cr;
+        } else {
+            capv[h] = (h ? sext_hi(H2[NV - 1]) : sext_lo(H2[NV - 1])) + oh;
+        }
+    };
+    auto step = [&](uint32_t t, auto masked_tag) {
+        constexpr bool MASKED = decltype(masked_tag)::value;
+        uint32_t top;
+        if (pass == 0) {
+            const int s0 = (init - ma) * (int)(t + 1);  // S(0, j)
+            top = ((uint32_t)(s0 - O[0]) & 0xFFFFu) | ((uint32_t)(s0 - O[1]) << 16);
+        } else {
+            const int ba = rdlane(bcur[0], t & 63u), bb = rdlane(bcur[1], t & 63u);
+            top = ((uint32_t)(ba - O[0]) & 0xFFFFu) | ((uint32_t)(bb - O[1]) << 16);
+        }
+        const uint32_t sh = (t & 3u) * 8;
+        const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
+        const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
+        const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
+        const uint32_t prev = recv;
+        recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
+        tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+
+        const int j = (int)t - lane + 1;
+        const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)M));
+        uint32_t acc0 = 0, acc1 = 0;
+        if (active) {
+            uint32_t GL = rep16(glg);
+            if (tdash) {
+                const int ga = ((tc2 & 0xFFFFu) == '-') ? gld : glg;
+                const int gb = ((tc2 >> 16) == '-') ? gld : glg;
+                GL = ((uint32_t)ga & 0xFFFFu) | ((uint32_t)gb << 16);
+            }
+            auto e_of = [&](int r) { return pk_min_u16(q2[r] ^ tc2, ONE); };
+            uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
+            uint32_t upv = recv;
+            static_for<0, R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                const uint32_t old = H2[r];
+                const uint32_t diag = dnext;
+                const uint32_t left = pk_add(old, GL);
+                if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
+                const uint32_t up = pk_add(upv, GUG);
+                const uint32_t m1 = pk_max(diag, left);
+                const uint32_t u = pk_max(m1, up);
+                if (CIGAR) {
+                    const uint32_t wd = pk_sub_sat(m1, up);
+                    const uint32_t wi = pk_sub_sat(diag, left);
+                    uint32_t& acc = (r < 8) ? acc0 : acc1;
+                    acc = bfi(0x01010101u << (7 - (r & 7)), sign_bytes(wd, wi), acc);
+                }
+                H2[r] = u;
+                upv = u;
+            });
+            if (MODE == kSemi && last_pass) {  // row n of each pair: H = S + ma*j, columns <= m_h, strict '>'
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int v = (h ? sext_hi(H2[NV - 1]) : sext_lo(H2[NV - 1])) + O[h] + ma * j;
+                    const bool better = j <= (int)io.m[h] && v > rb[h];
+                    rb[h] = better ? v : rb[h];
+                    rbj[h] = better ? (uint32_t)j : rbj[h];
+                }
+            }
+            if (has_next && (uint32_t)lane == nl - 1) {
+                io.B[2 * j] = sext_lo(H2[R - 1]) + O[0];
+                io.B[2 * j + 1] = sext_hi(H2[R - 1]) + O[1];
+            }
+        }
+        // column m_h reached by some lane this step (uniform window test)
+        if (t + 1 >= io.m[0] && t + 1 < io.m[0] + kWave) capture(0, j, active);
+        if (t + 1 >= io.m[1] && t + 1 < io.m[1] + kWave) capture(1, j, active);
+        if (CIGAR) {
+            const uint32_t off = (t * kWave + (uint32_t)lane) * 4u;
+            if (t < Tmax0) *(uint32_t*)((char*)prow0 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
+            if (t < Tmax1) *(uint32_t*)((char*)prow1 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
+        }
+    };
+    const uint32_t ramp_end = min(nl - 1, steps);
+    uint32_t t = 0, next_reload = 64;
+    auto run_steps = [&](uint32_t t_end, auto masked_tag) {
+        while (t < t_end) {
+            if (t == next_reload) {
+                reload(t);
+                next_reload += 64;
+            }
+            const uint32_t blk = min(t_end, next_reload);
+            for (; t < blk; ++t) step(t, masked_tag);
+        }
+    };
+    run_steps(ramp_end, std::true_type{});
+    run_steps(M, std::false_type{});
+    run_steps(steps, std::true_type{});
+
+    FlexOut out;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        PassOut& o = out.o[h];
+        o = PassOut{INT_MIN, 0, 0, INT_MIN, 0, 0};
+        if (MODE == kSemi) {
+            // column m_h: H = S + ma*m_h for every row, so S orders them; first lane, then first row
+            const int mx = wave_max(capv[h]);
+            const int fl = first_lane(capv[h] == mx && capv[h] != INT_MIN);
+            if (mx != INT_MIN) {
+                o.h = mx + ma * (int)io.m[h];
+                o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane(capr[h], fl) + 1;
+                o.j = io.m[h];
+            }
+            if (last_pass) {
+                o.row_h = rdlane(rb[h], nlh[h] - 1);  // INT_MIN: no column (m_h = 0 never reaches here)
+                o.row_j = (uint32_t)rdlane((int)rbj[h], nlh[h] - 1);
+            }
+        } else if (last_pass) {
+            o.corner = rdlane(capv[h], nlh[h] - 1) + ma * (int)io.m[h];
+        }
+    }
+    return out;
+}
+
+template <int MODE, bool CIGAR>
+__device__ __forceinline__ FlexOut flex_pass_nv(const FillArgs& a, const FlexIo& io, uint32_t pass, bool last_pass,
+                                                bool tdash, int lane) {
+    const uint32_t nrows = min((uint32_t)kPassRows, io.n[0] - pass * kPassRows);
+    const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
+    if (nv == kRows) return flex_pass<MODE, CIGAR, kRows>(a, io, pass, last_pass, tdash, lane);
+#define TA_NV_CASE(k) \
+    case k: return flex_pass<MODE, CIGAR, k>(a, io, pass, last_pass, tdash, lane);
+    switch (nv) {
+        TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
+        TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
+        default: TA_NV_CASE(15)
+    }
+#undef TA_NV_CASE
+}
+
+#ifndef TA_FLEX_WAVES
+#define TA_FLEX_WAVES 4
+#endif
+// flex_order: 2 pair ids per wave, pair A (larger n) first; same pass count and n mod 16
+template <int MODE, bool CIGAR>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_WAVES))) void flex_fill_kernel(FillArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t widx = wave_id();
+    if (widx >= a.count) return;
+    uint32_t p[2];
+    p[0] = a.order[2 * (a.begin + widx)];
+    p[1] = a.order[2 * (a.begin + widx) + 1];
+    FlexIo io;
+    bool tdash = false, qdash = false;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        io.n[h] = a.qlen[p[h]];
+        io.m[h] = a.tlen[p[h]];
+        io.Q[h] = a.qbytes + a.qoff[p[h]];
+        io.T[h] = a.tbytes + a.toff[p[h]];
+        io.ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
+        for (uint32_t k = (uint32_t)lane; k < io.m[h]; k += 64) tdash |= io.T[h][k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < io.n[h]; k += 64) qdash |= io.Q[h][k] == '-';
+    }
+    if (__ballot(qdash)) {  // per-row up gains: the int32 fill takes the couple
+        if (lane == 0) {
+            const uint32_t at = atomicAdd(a.fb_count, 2u);
+            a.fb_list[at] = p[0];
+            a.fb_list[at + 1] = p[1];
+        }
+        return;
+    }
+    tdash = __ballot(tdash) != 0;
+    const uint32_t passes = n_passes(io.n[0]);
+    io.B = (passes > 1) ? a.bnd + a.bnd_off[p[0]] : nullptr;
+    int best_h[2], corner[2] = {0, 0};
+    uint32_t best_i[2], best_j[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        best_h[h] = (MODE == kSemi) ? 0 : INT_MIN;
+        best_i[h] = 0;
+        best_j[h] = (MODE == kSemi) ? io.m[h] : 0;
+    }
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        const bool last_pass = pass + 1 == passes;
+        const FlexOut o = flex_pass_nv<MODE, CIGAR>(a, io, pass, last_pass, tdash, lane);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (MODE == kSemi && o.o[h].h > best_h[h]) {
+                best_h[h] = o.o[h].h;
+                best_i[h] = o.o[h].i;
+                best_j[h] = o.o[h].j;
+            }
+            if (MODE == kSemi && last_pass && o.o[h].row_h > best_h[h]) {
+                best_h[h] = o.o[h].row_h;
+                best_i[h] = io.n[h];
+                best_j[h] = o.o[h].row_j;
+            }
+            if (MODE == kGlobal && last_pass) corner[h] = o.o[h].corner;
+        }
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+    }
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t gi = (MODE == kGlobal) ? io.n[h] : best_i[h], gj = (MODE == kGlobal) ? io.m[h] : best_j[h];
+        if (lane == 0) {
+            a.score[p[h]] = (MODE == kGlobal) ? corner[h] : best_h[h];
+            a.target_begin[p[h]] = 0;
+            a.goal_i[p[h]] = gi;
+            a.goal_j[p[h]] = gj;
+        }
+    }
+}
+
+#endif  // TA_FLEX_MODE
+}  // namespace
+
+#ifdef TA_FLEX_MODE
+template <>
+hipError_t launch_flex_mode<TA_FLEX_MODE, (TA_FLEX_CIGAR != 0)>(const FillArgs& a, hipStream_t s) {
+    if (!a.count) return hipSuccess;
+    hipLaunchKernelGGL((flex_fill_kernel<TA_FLEX_MODE, TA_FLEX_CIGAR != 0>),
+                       dim3((a.count + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, s, a);
+    return hipGetLastError();
+}
+#endif
+
+}  // namespace ta

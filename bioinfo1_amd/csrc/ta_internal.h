@@ -109,6 +109,14 @@ template <int MODE, bool CIGAR>
 hipError_t launch_dual_mode(const FillArgs& a, hipStream_t s);
 // Can an n x m pair run in the packed int16 kernel without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
+// Flexible two-pair fill (ta_flex.hip, global / semi-global): a.order holds 2
+// pair ids per wave, the larger n first; both with the same pass count and
+// n mod 16; rebased int16 values, so any length fits.
+hipError_t launch_flex(int mode, bool cigar, const FillArgs& a, hipStream_t s);
+template <int MODE, bool CIGAR>
+hipError_t launch_flex_mode(const FillArgs& a, hipStream_t s);
+// Scoring whose rebased 16-bit values cannot overflow in the flexible fill.
+bool flex_fits(int mode, int match, int mismatch, int gap);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 
 }  // namespace ta

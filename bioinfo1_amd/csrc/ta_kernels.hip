@@ -462,6 +462,25 @@ hipError_t launch_dual(int mode, bool cigar, const FillArgs& a, hipStream_t s) {
     }
 }
 
+hipError_t launch_flex(int mode, bool cigar, const FillArgs& a, hipStream_t s) {
+    switch (mode * 2 + (cigar ? 1 : 0)) {
+        case 0: return launch_flex_mode<kGlobal, false>(a, s);
+        case 1: return launch_flex_mode<kGlobal, true>(a, s);
+        case 4: return launch_flex_mode<kSemi, false>(a, s);
+        case 5: return launch_flex_mode<kSemi, true>(a, s);
+        default: return hipErrorInvalidValue;
+    }
+}
+
+// The flexible fill keeps V = S - O within a wave's span: 1,024 rows + 2 x 64
+// columns of cells whose neighbours differ by at most |score| + |gap| <= 2*mag
+// (plus the 64-step drift between rebases).
+bool flex_fits(int mode, int ma, int mi, int gap) {
+    if (mode == kLocal) return false;
+    const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
+    return (kPassRows + 3LL * kWave) * 2 * mag * 2 <= 30000;
+}
+
 // Bounds of the biased 16-bit values of ta_dual.hip (S and every candidate),
 // with a margin; pairs that do not fit run in the int32 kernel.
 bool fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {

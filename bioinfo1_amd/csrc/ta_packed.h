@@ -1,0 +1,71 @@
+// bioinfo1_amd/csrc/ta_packed.h -- packed two-pair (2 x int16 per dword)
+// helpers shared by the dual fill (ta_dual.hip) and the flexible dual fill
+// (ta_flex.hip): v_pk_* arithmetic through clang vector builtins, the
+// sign-byte pointer-code packing and the branch-free select.
+#pragma once
+
+#include "ta_device.h"
+
+namespace ta {
+namespace {
+
+__device__ __forceinline__ uint32_t pk_add(uint32_t a, uint32_t b) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, a) + __builtin_bit_cast(s2, b));
+}
+__device__ __forceinline__ uint32_t pk_sub(uint32_t a, uint32_t b) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2, a) - __builtin_bit_cast(s2, b));
+}
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+    typedef short s2 __attribute__((ext_vector_type(2)));
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(s2, a), __builtin_bit_cast(s2, b)));
+}
+// max over v[B..E) as a balanced tree
+template <int B, int E>
+__device__ __forceinline__ uint32_t tree_max(const uint32_t* v) {
+    if constexpr (E - B == 1) return v[B];
+    else return pk_max(tree_max<B, (B + E) / 2>(v), tree_max<(B + E) / 2, E>(v));
+}
+// Packed helpers through clang vector builtins (inline asm costs an s_nop:
+// the hazard recognizer cannot see into it).  pk_min_u16 must get a
+// non-constant operand: min(x, 1) with a literal 1 is expanded into compares.
+typedef unsigned short u2 __attribute__((ext_vector_type(2)));
+typedef short s2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_min_u16(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_min(__builtin_bit_cast(u2, a), __builtin_bit_cast(u2, b)));
+}
+// a * b + c per half (v_pk_mad_u16: the low 16 bits are the same as i16)
+__device__ __forceinline__ uint32_t pk_mad_i16(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(s2v, a) * __builtin_bit_cast(s2v, b) + __builtin_bit_cast(s2v, c));
+}
+// a - b per half, saturating (v_pk_sub_i16 clamp): its sign bits (15, 31) are the per-half a < b
+__device__ __forceinline__ uint32_t pk_sub_sat(uint32_t a, uint32_t b) {
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(s2v, a), __builtin_bit_cast(s2v, b)));
+}
+// Pointer bits without lane masks: the sign bits of two compare words are
+// spread to whole bytes by v_perm_b32 (selectors 8..11 replicate the sign of
+// bytes 1, 3, 5, 7), giving [I_A, I_B, D_A, D_B] as 0x00/0xFF bytes, and one
+// bit-insert (v_bitop3_b32 on gfx950) drops them into bit (7 - r%8) of the
+// row group's accumulator.  The local-mode canonicalisation is two more
+// v_bitop3_b32, which hipcc forms from the logic expressions.
+constexpr uint32_t kSignBytes = 0x0B0A0908u;
+__device__ __forceinline__ uint32_t sign_bytes(uint32_t dword_d, uint32_t dword_i) {
+    return __builtin_amdgcn_perm(dword_d, dword_i, kSignBytes);
+}
+// v_bfi_b32 spelled out: from the C++ form hipcc builds and/or trees over
+// all 8 rows of a group, which keeps their sign bytes live (spills at 5 waves)
+__device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+    return r;
+}
+// 0xFFFF in each half whose sign bit (15 / 31) is set
+__device__ __forceinline__ uint32_t half_mask(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x09090808u); }
+__device__ __forceinline__ uint32_t rep16(int v) { return ((uint32_t)v & 0xFFFFu) | ((uint32_t)v << 16); }
+__device__ __forceinline__ int lo16(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
+__device__ __forceinline__ int hi16(uint32_t x) { return (int)(int16_t)(x >> 16); }
+
+
+}  // namespace
+}  // namespace ta

@@ -94,9 +94,13 @@ uint64_t ta_plan_cigar_slots_bytes(const ta_plan* plan);
 /* Device workspace held by the plan, and the number of launch chunks. */
 uint64_t ta_plan_workspace_bytes(const ta_plan* plan);
 uint32_t ta_plan_chunks(const ta_plan* plan);
-/* Pairs the plan runs in the packed two-pairs-per-wave int16 kernel (equal
- * lengths, scores provably within int16); the rest use the int32 kernel. */
+/* Pairs the plan runs in the packed two-pairs-per-wave int16 kernels (equal
+ * shapes with scores provably within int16, or -- global / semi-global --
+ * couples of different shapes in the rebased kernel); the rest use the int32
+ * kernel. */
 uint32_t ta_plan_dual_pairs(const ta_plan* plan);
+/* Of those, the pairs in couples of different shapes / beyond int16 (ta_flex.hip). */
+uint32_t ta_plan_flex_pairs(const ta_plan* plan);
 
 /* Device pointers for one execution of a plan. */
 typedef struct ta_device_io {

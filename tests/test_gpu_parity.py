@@ -242,3 +242,63 @@ def test_config5_shape_properties(aligner):
     meta, d = load_digest("cfg5_semi_sample")
     np.testing.assert_array_equal(r.scores[:32], d["scores"])
     np.testing.assert_array_equal(r.cigar_lens[:32], d["cigar_lens"])
+
+
+def _flex_batch(P, lo, hi, alphabet, seed, tdash=False, qdash=False):
+    """Ragged related pairs in groups that couple for the flexible dual fill
+    (same query pass count and length mod 16, different target lengths)."""
+    rng = np.random.default_rng(seed)
+    al = np.frombuffer(alphabet, np.uint8)
+    pairs = []
+    while len(pairs) < P:
+        n0 = int(rng.integers(lo, hi + 1))
+        for _ in range(2):
+            n = max(1, n0 - 16 * int(rng.integers(0, 4)))
+            if (n - 1) // 1024 != (n0 - 1) // 1024:
+                n = n0
+            m = max(1, int(n0 * rng.uniform(0.8, 1.2)))
+            q = al[rng.integers(len(al), size=n)]
+            t = q[: min(n, m)].copy()
+            flip = rng.random(t.shape[0]) < 0.1
+            t[flip] = al[rng.integers(len(al), size=int(flip.sum()))]
+            if m > t.shape[0]:
+                t = np.concatenate([t, al[rng.integers(len(al), size=m - t.shape[0])]])
+            if tdash and len(pairs) % 3 == 0:
+                t[rng.integers(m, size=max(1, m // 50))] = ord("-")
+            if qdash and len(pairs) % 5 == 0:
+                q = q.copy()
+                q[rng.integers(n, size=1)] = ord("-")
+            pairs.append((q.tobytes(), t.tobytes()))
+    return synth.from_pairs(pairs[:P])
+
+
+FLEX_FUZZ = [
+    # (mode, scoring, alphabet, lo, hi, n_pairs, tdash, qdash)
+    (0, (1, -1, -1), b"ACGT", 1, 300, 120, False, False),
+    (2, (1, -1, -1), b"ACGT", 1, 300, 120, False, False),
+    (0, (2, -3, -2), b"ACGT", 900, 2200, 24, True, False),
+    (2, (2, -3, -2), b"ACGT", 900, 2200, 24, True, True),
+    (2, (3, -2, 0), b"ACGTN", 1000, 1100, 16, False, False),
+    (0, (2, -1, 2), b"AC", 500, 1500, 20, False, False),
+    (2, (1, -1, -1), b"ACGT", 10700, 12500, 6, False, False),   # beyond absolute int16: rebasing
+    (0, (1, -1, -1), b"ACGT", 10700, 11200, 4, False, False),
+]
+
+
+@pytest.mark.parametrize("case", range(len(FLEX_FUZZ)))
+def test_flex_fuzz(aligner, oracle, case, monkeypatch):
+    mode, sc, alpha, lo, hi, P, td, qd = FLEX_FUZZ[case]
+    b = _flex_batch(P, lo, hi, alpha, 0xF1E0 + case, td, qd)
+    plan = DevicePlan(aligner, b, mode, *sc, True)
+    assert plan.flex_pairs >= P // 3, (plan.flex_pairs, plan.dual_pairs)
+    plan.close()
+    want = oracle.align_batch(b, mode, *sc, True)
+    for flex in ("1", "0"):
+        monkeypatch.setenv("TA_FLEX", flex)
+        for cig in (True, False):
+            got = aligner.align_batch(b, mode, *sc, cig)
+            np.testing.assert_array_equal(got.scores, want.scores)
+            np.testing.assert_array_equal(got.target_begins, want.target_begins)
+            if cig:
+                for p in range(P):
+                    assert got.cigar(p) == want.cigar(p), (case, flex, p, b.qlen[p], b.tlen[p])
