@@ -237,7 +237,7 @@ def main_mapper(args):
     sc = tuple(int(x) for x in args.scoring.split(","))
     g = synth.genome(synth.ECOLI_LEN)
     rs = synth.ont_reads(args.pairs, g, first_read=rank * args.pairs)
-    reads = [rs.read(r) for r in range(rs.n_reads)]
+    reads = (rs.bytes if rs.bytes.size else np.zeros(1, np.uint8), rs.off.copy(), rs.len.copy())  # SoA, packed once
     mp = M.Mapper(dev_index)
     t0 = time.perf_counter()
     idx = M.Index(mp, "ecoli_syn", g.tobytes(), 15, 5, 0.001)

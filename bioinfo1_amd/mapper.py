@@ -94,6 +94,9 @@ def _check(r, ctx=None):
 
 
 def _soa(seqs):
+    """(bytes uint8[], off uint64[], len uint32[]) -- also accepts that tuple as is."""
+    if isinstance(seqs, tuple) and len(seqs) == 3 and isinstance(seqs[0], np.ndarray):
+        return seqs
     seqs = [bytes(s) for s in seqs]
     ln = np.array([len(s) for s in seqs], dtype=np.uint32)
     off = np.zeros(len(seqs), dtype=np.uint64)
@@ -101,6 +104,11 @@ def _soa(seqs):
         off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
     b = np.frombuffer(b"".join(seqs) or b"\0", dtype=np.uint8).copy()
     return b, off, ln
+
+
+def soa(seqs):
+    """Pack sequences once into the SoA layout map_batch takes."""
+    return _soa(seqs)
 
 
 class Mapper:
@@ -229,6 +237,7 @@ class Index:
                         [x.value for x in v]))
 
     def map_batch(self, reads, opt: Options) -> MapResult:
+        """reads: sequences, or a prepared (bytes, off, len) tuple (see soa())."""
         L = lib()
         b, off, ln = _soa(reads)
         n = len(ln)
