@@ -22,6 +22,10 @@ struct ta_context {
     // its packed two-pair fill; the caller's stream waits for it (fork / join)
     hipStream_t aux = nullptr, aux2 = nullptr;  // aux2: the equal-shape dual fill beside the flexible one
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
+    // staged plans: tracebacks on their own stream, one event per stage
+    hipStream_t tbs = nullptr;
+    hipEvent_t ev_tb_done = nullptr;
+    std::vector<hipEvent_t> ev_stage;
     std::string last_error;
     std::mutex mu;  // one batch at a time per context
     // grow-only device staging for ta_align_batch
@@ -34,6 +38,7 @@ struct ta_context {
     // context and grown at execute time (a plan's chunks are sized by its
     // budget): plans of one context must not execute concurrently.
     Buf ws_ptrs, ws_bnd;
+    uint32_t epoch = 0;  // flexible-fill launches so far (tags of their pass hand-off records)
 };
 
 struct ta_plan {
@@ -48,7 +53,9 @@ struct ta_plan {
     bool fused = true;
     bool dual = true;   // packed two-pair int16 fill where it fits (TA_DUAL=0 disables)
     bool flex = true;   // ... also for couples of different shapes / long pairs (TA_FLEX=0 disables)
+    bool staged = false;  // chunks use disjoint workspace: traceback k overlaps fill k+1
     std::vector<uint32_t> qlen, tlen, order, singles, duals, flexes;
+    std::vector<uint32_t> flex_task_off;  // per flex couple: first task (one per query pass); + total
     std::vector<uint64_t> slot_off;
     struct Chunk {
         uint32_t begin, count;    // all pairs (traceback order)
@@ -67,6 +74,8 @@ struct ta_plan {
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
     uint32_t *d_goal_i = nullptr, *d_goal_j = nullptr;
     uint32_t* d_fb = nullptr;  // dual fallback: [n_dual_pairs] list, then one counter per chunk
+    uint32_t *d_flex_task_off = nullptr, *d_tickets = nullptr, *d_err = nullptr;
+    void* d_pout = nullptr;  // PassOut[2] per flex task
 };
 
 namespace {
@@ -149,6 +158,8 @@ int ta_context_create(int device, ta_context** out) {
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->tbs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_tb_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
@@ -168,6 +179,9 @@ void ta_context_destroy(ta_context* ctx) {
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
     if (ctx->aux2) (void)hipStreamDestroy(ctx->aux2);
+    if (ctx->tbs) (void)hipStreamDestroy(ctx->tbs);
+    if (ctx->ev_tb_done) (void)hipEventDestroy(ctx->ev_tb_done);
+    for (hipEvent_t e : ctx->ev_stage) (void)hipEventDestroy(e);
     if (ctx->ev_join2) (void)hipEventDestroy(ctx->ev_join2);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
@@ -179,7 +193,7 @@ void ta_plan_destroy(ta_plan* pl) {
     (void)hipSetDevice(pl->ctx->device);
     for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_flexes, (void*)pl->d_ptr_off,
                     (void*)pl->d_bnd_off, (void*)pl->d_slot_off, (void*)pl->d_goal_i, (void*)pl->d_goal_j,
-                    (void*)pl->d_fb})
+                    (void*)pl->d_fb, (void*)pl->d_flex_task_off, (void*)pl->d_tickets, (void*)pl->d_err, pl->d_pout})
         if (p) (void)hipFree(p);
     delete pl;
 }
@@ -267,7 +281,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
         });
         for (size_t i = 0; i < cand.size();) {
             const uint32_t A = cand[i];
-            if (i + 1 < cand.size() && key(cand[i + 1]) == key(A)) {
+            if (i + 1 < cand.size() && key(cand[i + 1]) == key(A) && ta::n_passes(pl->qlen[A]) < 64) {
                 const uint32_t B = cand[i + 1];
                 const uint64_t M = std::max(pl->tlen[A], pl->tlen[B]);
                 const uint64_t wave = (uint64_t)pl->qlen[A] * M;
@@ -278,7 +292,8 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
                     continue;
                 }
             }
-            units.push_back({0, A, A, (uint64_t)pl->qlen[A] * pl->tlen[A]});
+            const uint32_t ps = ta::n_passes(pl->qlen[A]);
+            units.push_back({ps >= 4 && ps < 64 ? 2 : 0, A, A, (uint64_t)pl->qlen[A] * pl->tlen[A]});
             ++i;
         }
     } else {
@@ -286,32 +301,55 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     }
     std::stable_sort(units.begin(), units.end(), [](const Unit& x, const Unit& y) { return x.cost > y.cost; });
     pl->order.clear();
+    // Staging: when the whole plan's codes fit the budget and the traceback runs
+    // as its own kernel (packed couples), cut it into TA_STAGES chunks with
+    // disjoint workspace, so stage k's traceback (SALU-bound) runs on a stream
+    // of its own beside stage k+1's fill (VALU-bound).
+    uint64_t total_pd = 0;
+    bool any_couple = false;
+    for (const Unit& u : units) {
+        total_pd += !pl->want_cigar ? 0 : ta::ptr_dwords(pl->qlen[u.a], pl->tlen[u.a]) +
+                                             (u.kind ? ta::ptr_dwords(pl->qlen[u.b], pl->tlen[u.b]) : 0);
+        any_couple |= u.kind != 0;
+    }
+    uint32_t stages = 1;  // off by default: a quarter-size fill launch runs far below the full one (r01l: 2 stages 2,267 vs 2,812 GCUPS)
+    if (const char* e = std::getenv("TA_STAGES")) stages = (uint32_t)std::max(1, std::atoi(e));
+    pl->staged = pl->want_cigar && any_couple && total_pd <= budget_dw && stages > 1 && units.size() >= 8ull * stages;
+    const size_t per_stage = pl->staged ? (units.size() + stages - 1) / stages : units.size();
     ta_plan::Chunk cur{};
     uint32_t couples_before = 0;
+    uint64_t off_pd = 0, off_bw = 0;  // running offsets (reset per chunk unless staged)
     auto open_chunk = [&]() {
         cur = ta_plan::Chunk{(uint32_t)pl->order.size(), 0, (uint32_t)pl->singles.size(), 0,
                              (uint32_t)(pl->duals.size() / 2), 0, (uint32_t)(pl->flexes.size() / 2), 0,
                              couples_before, 0, 0};
+        if (!pl->staged) off_pd = off_bw = 0;
     };
     open_chunk();
-    for (const Unit& u : units) {
+    for (size_t k = 0; k < units.size(); ++k) {
+        const Unit& u = units[k];
         const uint32_t na = pl->qlen[u.a], ma = pl->tlen[u.a], nb = pl->qlen[u.b], mb = pl->tlen[u.b];
-        const uint64_t pd = !pl->want_cigar ? 0 : ta::ptr_dwords(na, ma) + (u.kind ? ta::ptr_dwords(nb, mb) : 0);
-        if (cur.count && cur.ptr_dwords + pd > budget_dw) {
+        const uint64_t pd = !pl->want_cigar ? 0 : ta::ptr_dwords(na, ma) + (u.kind && u.a != u.b ? ta::ptr_dwords(nb, mb) : 0);
+        if (cur.count && (pl->staged ? k % per_stage == 0 : cur.ptr_dwords + pd > budget_dw)) {
             pl->chunks.push_back(cur);
             open_chunk();
         }
         const uint32_t q[2] = {u.a, u.b};
-        for (int h = 0; h < (u.kind ? 2 : 1); ++h) {
+        const int halves = (u.kind && u.a != u.b) ? 2 : 1;
+        for (int h = 0; h < halves; ++h) {
             const uint32_t x = q[h];
-            ptr_off[x] = cur.ptr_dwords;
-            bnd_off[x] = cur.bnd_words;
-            cur.ptr_dwords += pl->want_cigar ? ta::ptr_dwords(pl->qlen[x], pl->tlen[x]) : 0;
+            ptr_off[x] = off_pd;
+            bnd_off[x] = off_bw;
+            const uint64_t xd = pl->want_cigar ? ta::ptr_dwords(pl->qlen[x], pl->tlen[x]) : 0;
             // flex: pair A holds both pairs' absolute int32 boundary rows, interleaved;
             // each pair keeps a region of its own for the int32 fallback ('-' in a query)
             uint64_t bw = ta::bnd_words(pl->qlen[x], pl->tlen[x]);
             if (u.kind == 2 && h == 0 && ta::n_passes(na) > 1)
-                bw = std::max<uint64_t>(bw, 2ull * ((uint64_t)std::max(ma, mb) + 1 + ta::kWave));
+                bw = std::max<uint64_t>(bw, 8ull * ((uint64_t)std::max(ma, mb) + 1));
+            bw += bw & 1;  // keep every region 8-byte aligned (64-bit hand-off records)
+            off_pd += xd;
+            off_bw += bw;
+            cur.ptr_dwords += xd;
             cur.bnd_words += bw;
             pl->order.push_back(x);
         }
@@ -331,13 +369,21 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
             pl->n_dual_pairs += 2;
             ++couples_before;
         }
-        cur.count += u.kind ? 2 : 1;
+        cur.count += (u.kind && u.a != u.b) ? 2 : 1;
     }
     if (cur.count) pl->chunks.push_back(cur);
     if (pl->n_dual_pairs) pl->fused = false;
-    for (auto& c : pl->chunks) {
-        pl->ws_ptr_dwords = std::max(pl->ws_ptr_dwords, c.ptr_dwords);
-        pl->ws_bnd_words = std::max(pl->ws_bnd_words, c.bnd_words);
+    pl->flex_task_off.assign(1, 0);
+    for (size_t w = 0; w < pl->flexes.size() / 2; ++w)
+        pl->flex_task_off.push_back(pl->flex_task_off.back() + ta::n_passes(pl->qlen[pl->flexes[2 * w]]));
+    if (pl->staged) {
+        pl->ws_ptr_dwords = off_pd;
+        pl->ws_bnd_words = off_bw;
+    } else {
+        for (auto& c : pl->chunks) {
+            pl->ws_ptr_dwords = std::max(pl->ws_ptr_dwords, c.ptr_dwords);
+            pl->ws_bnd_words = std::max(pl->ws_bnd_words, c.bnd_words);
+        }
     }
     int rc = TA_OK;
     auto up = [&](int r) {
@@ -349,6 +395,13 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     up(upload(ctx, &pl->d_singles, pl->singles));
     up(upload(ctx, &pl->d_duals, pl->duals));
     up(upload(ctx, &pl->d_flexes, pl->flexes));
+    if (!pl->flexes.empty()) {
+        up(upload(ctx, &pl->d_flex_task_off, pl->flex_task_off));
+        up(upload(ctx, &pl->d_tickets, std::vector<uint32_t>(pl->chunks.size(), 0u)));
+        up(upload(ctx, &pl->d_err, std::vector<uint32_t>(1, 0u)));
+        if (rc == TA_OK && hipMalloc(&pl->d_pout, pl->flex_task_off.back() * 48ull + 16) != hipSuccess)
+            rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc flex pass results");
+    }
     up(upload(ctx, &pl->d_ptr_off, ptr_off));
     up(upload(ctx, &pl->d_bnd_off, bnd_off));
     up(upload(ctx, &pl->d_slot_off, pl->slot_off));
@@ -452,6 +505,13 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
                 d.count = ch.fcount;
                 d.fb_list = fb_list;
                 d.fb_count = fb_count;
+                d.task_off = pl->d_flex_task_off;
+                d.ticket = pl->d_tickets + c;
+                d.n_tasks = pl->flex_task_off[ch.fbegin + ch.fcount] - pl->flex_task_off[ch.fbegin];
+                d.epoch = ++ctx->epoch & 0x3FFFFFFu;
+                d.err = pl->d_err;
+                d.pout = pl->d_pout;
+                TA_HIP(ctx, hipMemsetAsync(d.ticket, 0, 4, s));
                 TA_HIP(pl->ctx, ta::launch_flex(pl->type, pl->want_cigar, d, s));
             }
             if (ch.dcount && ch.fcount) TA_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_join2, 0));
@@ -502,8 +562,28 @@ int ta_plan_execute(ta_plan* pl, const ta_device_io* io, void* stream) {
     if (int r = check_io(pl, io)) return r;
     TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
     hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
-    for (uint32_t c = 0; c < pl->chunks.size(); ++c)
-        if (int r = exec_chunk(pl, io, s, c, true, true)) return r;
+    ta_context* ctx = pl->ctx;
+    if (!pl->staged) {
+        for (uint32_t c = 0; c < pl->chunks.size(); ++c)
+            if (int r = exec_chunk(pl, io, s, c, true, true)) return r;
+        return TA_OK;
+    }
+    // fills back to back on the caller's stream; stage c's traceback on tbs once its fill is done
+    while (ctx->ev_stage.size() < pl->chunks.size()) {
+        hipEvent_t e = nullptr;
+        TA_HIP(ctx, hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        ctx->ev_stage.push_back(e);
+    }
+    TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
+    TA_HIP(ctx, hipStreamWaitEvent(ctx->tbs, ctx->ev_fork, 0));  // tracebacks after earlier work on s
+    for (uint32_t c = 0; c < pl->chunks.size(); ++c) {
+        if (int r = exec_chunk(pl, io, s, c, true, false)) return r;
+        TA_HIP(ctx, hipEventRecord(ctx->ev_stage[c], s));
+        TA_HIP(ctx, hipStreamWaitEvent(ctx->tbs, ctx->ev_stage[c], 0));
+        if (int r = exec_chunk(pl, io, ctx->tbs, c, false, true)) return r;
+    }
+    TA_HIP(ctx, hipEventRecord(ctx->ev_tb_done, ctx->tbs));
+    TA_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_tb_done, 0));
     return TA_OK;
 }
 

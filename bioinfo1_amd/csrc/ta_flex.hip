@@ -34,22 +34,55 @@ namespace {
 __device__ __forceinline__ int sext_lo(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 __device__ __forceinline__ int sext_hi(uint32_t x) { return (int)(int16_t)(x >> 16); }
 
+// global-address-space view for the hand-off records (agent-scope atomics on
+// global pointers: sc1 loads / stores, never flat)
+typedef __attribute__((address_space(1))) unsigned long long gu64;
+
 struct FlexIo {
     const uint8_t* Q[2];
     const uint8_t* T[2];
     uint32_t* ptrs[2];
-    int32_t* B;  // boundary row: absolute S per column and pair, [2*j + h]
     uint32_t n[2], m[2];
+    // Pass hand-off (each pass of a couple runs on its own wave): the bottom
+    // row of pass p goes to 8-byte records rec_w[2*j + h] = tag << 32 |
+    // absolute S (the data is its own flag: MI355X guide, Guideline 16 R2),
+    // written with relaxed agent-scope (sc1) stores; pass p+1 polls a chunk
+    // of 64 columns with sc1 loads until every record carries the tag it
+    // expects.  Two buffers alternate by pass parity: pass p+2 overwrites
+    // column j only after pass p+1 has written its own column j, i.e. long
+    // after pass p+1 read column j of pass p.
+    uint64_t* rec_w;        // this pass's bottom row (null on the last pass)
+    const uint64_t* rec_r;  // the previous pass's (null on pass 0)
+    uint32_t tag_w, tag_r;
+    uint32_t* err;
 };
 
 struct FlexOut {
     PassOut o[2];
 };
 
-// 64 columns per chunk of the absolute boundary row, pair h
-__device__ __forceinline__ int load_bchunk2(const int32_t* B, uint32_t M, uint32_t k, int lane, int h) {
+// 64 columns per chunk of the previous pass's bottom row (absolute S, both
+// pairs); polls (bounded) until the producing wave has written all of them
+__device__ __forceinline__ void load_rec_chunk(const FlexIo& io, uint32_t M, uint32_t k, int lane, int (&v)[2]) {
     const uint32_t j = k * 64u + (uint32_t)lane + 1u;
-    return j <= M ? B[2 * j + h] : 0;
+    const gu64* r = (const gu64*)(io.rec_r + 2ull * j);
+    for (uint32_t spins = 0;; ++spins) {
+        bool ok = true;
+        v[0] = v[1] = 0;
+        if (j <= M) {
+            const uint64_t x = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t y = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(x >> 32) == io.tag_r && (uint32_t)(y >> 32) == io.tag_r;
+            v[0] = (int)(uint32_t)x;
+            v[1] = (int)(uint32_t)y;
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spins > (1u << 22)) {  // bounded: the kernel always ends
+            if (lane == 0) atomicOr(io.err, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
 }
 
 template <int MODE, bool CIGAR, int NV>
@@ -96,11 +129,8 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     }
     int bcur[2] = {0, 0}, bnext[2] = {0, 0};
     if (pass > 0) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            bcur[h] = load_bchunk2(io.B, M, 0, lane, h);
-            bnext[h] = load_bchunk2(io.B, M, 1, lane, h);
-        }
+        load_rec_chunk(io, M, 0, lane, bcur);
+        load_rec_chunk(io, M, 1, lane, bnext);
     }
     const uint32_t steps = M + nl - 1;
     const uint32_t Tmax0 = pass_steps(io.m[0]), Tmax1 = pass_steps(io.m[1]);
@@ -116,11 +146,9 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             }
         }
         if (pass > 0) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                bcur[h] = bnext[h];
-                bnext[h] = load_bchunk2(io.B, M, (t >> 6) + 1, lane, h);
-            }
+            bcur[0] = bnext[0];
+            bcur[1] = bnext[1];
+            load_rec_chunk(io, M, (t >> 6) + 1, lane, bnext);
         }
         // rebase (every 64 steps, all lanes alike): a lane that holds current cells
         const uint32_t d = (uint32_t)rdlane((int)H2[0], t < M ? 0u : nl - 1);
@@ -210,8 +238,12 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 }
             }
             if (has_next && (uint32_t)lane == nl - 1) {
-                io.B[2 * j] = sext_lo(H2[R - 1]) + O[0];
-                io.B[2 * j + 1] = sext_hi(H2[R - 1]) + O[1];
+                const uint64_t tg = (uint64_t)io.tag_w << 32;
+                gu64* wr = (gu64*)(io.rec_w + 2ull * j);
+                __hip_atomic_store(wr, tg | (uint32_t)(sext_lo(H2[R - 1]) + O[0]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(wr + 1, tg | (uint32_t)(sext_hi(H2[R - 1]) + O[1]), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         // column m_h reached by some lane this step (uniform window test)
@@ -283,15 +315,31 @@ __device__ __forceinline__ FlexOut flex_pass_nv(const FillArgs& a, const FlexIo&
 #ifndef TA_FLEX_WAVES
 #define TA_FLEX_WAVES 4
 #endif
-// flex_order: 2 pair ids per wave, pair A (larger n) first; same pass count and n mod 16
+constexpr uint32_t kSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to the int32 fill
+
+// One wave per (couple, pass).  flex order: 2 pair ids per couple, pair A
+// (larger n) first; same pass count and n mod 16 (a single long pair may be
+// coupled with itself).  A wave takes the next ticket; tasks are numbered
+// couple by couple, pass by pass, so pass p-1 of its couple belongs to a wave
+// that took an earlier ticket and is running: every poll ends.
 template <int MODE, bool CIGAR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_WAVES))) void flex_fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint32_t widx = wave_id();
-    if (widx >= a.count) return;
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(a.ticket, 1u);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+    if (tk >= a.n_tasks) return;
+    const uint32_t g = a.task_off[a.begin] + tk;  // plan-global task index
+    uint32_t lo = a.begin, hi = a.begin + a.count;  // couple: last w with task_off[w] <= g
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a.task_off[mid] <= g) lo = mid;
+        else hi = mid;
+    }
+    const uint32_t w = lo, pass = g - a.task_off[w];
     uint32_t p[2];
-    p[0] = a.order[2 * (a.begin + widx)];
-    p[1] = a.order[2 * (a.begin + widx) + 1];
+    p[0] = a.order[2 * w];
+    p[1] = a.order[2 * w + 1];
     FlexIo io;
     bool tdash = false, qdash = false;
 #pragma unroll
@@ -304,53 +352,72 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
         for (uint32_t k = (uint32_t)lane; k < io.m[h]; k += 64) tdash |= io.T[h][k] == '-';
         for (uint32_t k = (uint32_t)lane; k < io.n[h]; k += 64) qdash |= io.Q[h][k] == '-';
     }
-    if (__ballot(qdash)) {  // per-row up gains: the int32 fill takes the couple
+    PassOut* po = static_cast<PassOut*>(a.pout) + 2ull * g;
+    if (__ballot(qdash)) {  // per-row up gains: the int32 fill takes the couple (pass 0's wave hands it over)
         if (lane == 0) {
-            const uint32_t at = atomicAdd(a.fb_count, 2u);
-            a.fb_list[at] = p[0];
-            a.fb_list[at + 1] = p[1];
+            if (pass == 0) {
+                const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
+                const uint32_t at = atomicAdd(a.fb_count, k);
+                a.fb_list[at] = p[0];
+                if (k == 2) a.fb_list[at + 1] = p[1];
+            }
+            po[0].i = kSkip;
+            po[1].i = kSkip;
         }
         return;
     }
     tdash = __ballot(tdash) != 0;
     const uint32_t passes = n_passes(io.n[0]);
-    io.B = (passes > 1) ? a.bnd + a.bnd_off[p[0]] : nullptr;
-    int best_h[2], corner[2] = {0, 0};
-    uint32_t best_i[2], best_j[2];
+    const bool last_pass = pass + 1 == passes;
+    const uint32_t M = max(io.m[0], io.m[1]);
+    uint64_t* rec = reinterpret_cast<uint64_t*>(a.bnd + a.bnd_off[p[0]]);  // 2 buffers x 2(M+1) records
+    const uint64_t rb = 2ull * (M + 1);
+    io.rec_w = last_pass ? nullptr : rec + (pass & 1u) * rb;
+    io.rec_r = pass ? rec + ((pass - 1u) & 1u) * rb : nullptr;
+    io.tag_w = a.epoch * 64u + pass + 1u;  // never 0, unique per launch and pass
+    io.tag_r = a.epoch * 64u + pass;
+    io.err = a.err;
+    const FlexOut o = flex_pass_nv<MODE, CIGAR>(a, io, pass, last_pass, tdash, lane);
+    if (lane == 0) {
+        po[0] = o.o[0];
+        po[1] = o.o[1];
+    }
+}
+
+// After the fill: fold each couple's per-pass results in pass order (the
+// upper pass wins ties; semi: row n after column m, :265-278).
+template <int MODE>
+__global__ void flex_combine_kernel(FillArgs a) {
+    const uint32_t w = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= a.begin + a.count) return;
+    const uint32_t g0 = a.task_off[w], passes = a.task_off[w + 1] - g0;
+    const PassOut* po = static_cast<const PassOut*>(a.pout) + 2ull * g0;
+    if (po[0].i == kSkip) return;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        best_h[h] = (MODE == kSemi) ? 0 : INT_MIN;
-        best_i[h] = 0;
-        best_j[h] = (MODE == kSemi) ? io.m[h] : 0;
-    }
-    for (uint32_t pass = 0; pass < passes; ++pass) {
-        const bool last_pass = pass + 1 == passes;
-        const FlexOut o = flex_pass_nv<MODE, CIGAR>(a, io, pass, last_pass, tdash, lane);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (MODE == kSemi && o.o[h].h > best_h[h]) {
-                best_h[h] = o.o[h].h;
-                best_i[h] = o.o[h].i;
-                best_j[h] = o.o[h].j;
+        const uint32_t p = a.order[2 * w + h];
+        const uint32_t n = a.qlen[p], m = a.tlen[p];
+        int best_h = (MODE == kSemi) ? 0 : INT_MIN, corner = 0;
+        uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
+        for (uint32_t k = 0; k < passes; ++k) {
+            const PassOut& o = po[2 * k + h];
+            if (MODE == kSemi && o.h > best_h) {
+                best_h = o.h;
+                best_i = o.i;
+                best_j = o.j;
             }
-            if (MODE == kSemi && last_pass && o.o[h].row_h > best_h[h]) {
-                best_h[h] = o.o[h].row_h;
-                best_i[h] = io.n[h];
-                best_j[h] = o.o[h].row_j;
+            if (MODE == kSemi && k + 1 == passes && o.row_h > best_h) {
+                best_h = o.row_h;
+                best_i = n;
+                best_j = o.row_j;
             }
-            if (MODE == kGlobal && last_pass) corner[h] = o.o[h].corner;
+            if (MODE == kGlobal && k + 1 == passes) corner = o.corner;
         }
-        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        const uint32_t gi = (MODE == kGlobal) ? io.n[h] : best_i[h], gj = (MODE == kGlobal) ? io.m[h] : best_j[h];
-        if (lane == 0) {
-            a.score[p[h]] = (MODE == kGlobal) ? corner[h] : best_h[h];
-            a.target_begin[p[h]] = 0;
-            a.goal_i[p[h]] = gi;
-            a.goal_j[p[h]] = gj;
-        }
+        if (h == 1 && p == a.order[2 * w]) break;  // a pair coupled with itself
+        a.score[p] = (MODE == kGlobal) ? corner : best_h;
+        a.target_begin[p] = 0;
+        a.goal_i[p] = (MODE == kGlobal) ? n : best_i;
+        a.goal_j[p] = (MODE == kGlobal) ? m : best_j;
     }
 }
 
@@ -361,8 +428,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
 template <>
 hipError_t launch_flex_mode<TA_FLEX_MODE, (TA_FLEX_CIGAR != 0)>(const FillArgs& a, hipStream_t s) {
     if (!a.count) return hipSuccess;
-    hipLaunchKernelGGL((flex_fill_kernel<TA_FLEX_MODE, TA_FLEX_CIGAR != 0>),
-                       dim3((a.count + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, s, a);
+    if (a.n_tasks)
+        hipLaunchKernelGGL((flex_fill_kernel<TA_FLEX_MODE, TA_FLEX_CIGAR != 0>),
+                           dim3((a.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL((flex_combine_kernel<TA_FLEX_MODE>), dim3((a.count + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 #endif

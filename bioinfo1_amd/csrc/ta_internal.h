@@ -71,6 +71,14 @@ struct FillArgs {
     uint32_t* fb_list;
     uint32_t* fb_count;
     const uint32_t* count_dev;
+    // flexible fill, one wave per (couple, pass): waves take tickets in launch
+    // order, so every pass a wave waits on is already held by a running wave
+    const uint32_t* task_off;  // per flex couple (plan order): its first task; [w + 1] - [w] = passes
+    uint32_t* ticket;          // this launch's ticket counter (zeroed before the launch)
+    uint32_t n_tasks;          // tasks of this launch
+    uint32_t epoch;            // tag base of this launch's pass hand-off records
+    uint32_t* err;             // a poll gave up (never on a correct schedule)
+    void* pout;                // PassOut[2] per task (plan-global task index)
 };
 
 struct TraceArgs {

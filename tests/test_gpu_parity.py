@@ -163,9 +163,10 @@ def test_related_long_pairs(aligner, oracle):
         np.testing.assert_array_equal(want.scores, got.scores)
 
 
-def test_device_plan_and_chunking(aligner):
+def test_device_plan_and_chunking(aligner, monkeypatch):
     import torch
 
+    monkeypatch.setenv("TA_STAGES", "1")  # no staging: one chunk when the budget holds everything
     b = synth.uniform_batch(300, 1000, 1000, seed=11)
     host = aligner.align_batch(b, 1, 1, -1, -1, True)
     for budget in (0, 3 * 1063 * 256):  # default, and ~3 pairs per chunk
@@ -282,6 +283,8 @@ FLEX_FUZZ = [
     (0, (2, -1, 2), b"AC", 500, 1500, 20, False, False),
     (2, (1, -1, -1), b"ACGT", 10700, 12500, 6, False, False),   # beyond absolute int16: rebasing
     (0, (1, -1, -1), b"ACGT", 10700, 11200, 4, False, False),
+    (2, (1, -1, -1), b"ACGT", 4100, 6000, 3, False, False),     # odd groups: long singles coupled with themselves
+    (0, (2, -3, -2), b"ACGT", 4100, 6000, 5, True, True),
 ]
 
 
@@ -302,3 +305,24 @@ def test_flex_fuzz(aligner, oracle, case, monkeypatch):
             if cig:
                 for p in range(P):
                     assert got.cigar(p) == want.cigar(p), (case, flex, p, b.qlen[p], b.tlen[p])
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_staged_plans(aligner, oracle, monkeypatch, mode):
+    """Staged plans (traceback of stage k on its own stream beside the fill of
+    stage k+1, disjoint workspace) give the same bytes as unstaged ones."""
+    import torch
+
+    b = synth.related_batch(400, 300, 300, seed=21 + mode)
+    want = oracle.align_batch(b, mode, 1, -1, -1, True)
+    for st in ("1", "3", "4"):
+        monkeypatch.setenv("TA_STAGES", st)
+        plan = DevicePlan(aligner, b, mode, 1, -1, -1, True)
+        assert plan.chunks == (1 if st == "1" else int(st))
+        for _ in range(2):
+            plan.run()
+        torch.cuda.synchronize()
+        r = plan.results()
+        np.testing.assert_array_equal(r.scores, want.scores)
+        assert r.cigars() == want.cigars()
+        plan.close()
