@@ -252,9 +252,12 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     };
     std::vector<Unit> units;
     std::vector<uint32_t> rest;
+    const bool flex_ok = pl->dual && pl->flex && ta::flex_fits(type, match, mismatch, gap);
     for (uint32_t k = 0; k < n_pairs;) {
         const uint32_t p = pl->order[k];
         const uint32_t n = pl->qlen[p], m = pl->tlen[p];
+        // (equal shapes within int16 stay on the dual fill even when multi-pass: measured faster
+        // than the pipelined flexible fill on config 5, 4,056 vs 3,765 GCUPS)
         const bool couple = pl->dual && k + 1 < n_pairs && pl->qlen[pl->order[k + 1]] == n &&
                             pl->tlen[pl->order[k + 1]] == m && ta::fits_int16(type, n, m, match, mismatch, gap);
         if (couple) {
@@ -265,7 +268,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
             ++k;
         }
     }
-    if (pl->dual && pl->flex && ta::flex_fits(type, match, mismatch, gap)) {
+    if (flex_ok) {
         // flexible couples: same pass count and n mod 16 (same rows in the last
         // lane), neighbours by (n, m), at most 25 % of the wave's cells wasted
         std::vector<uint32_t> cand;
