@@ -74,6 +74,9 @@ def parse():
     ap.add_argument("--workspace-gb", type=float, default=0.0,
                     help="device budget (GB) for the 2-bit traceback codes; 0 = the library default (85%% of free HBM); batches above it run in chunks")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--gap-open", type=int, default=None,
+                    help="affine-gap extension (no reference counterpart): a gap of length L costs "
+                         "gap_open + L*gap, gap = the third --scoring value (config 5's 'affine gaps')")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal only)")
     a = ap.parse_args()
     if a.workload == "cfg2":
@@ -88,39 +91,59 @@ def parse():
         a.mode = a.mode or "semiGlobal"
         a.qlen = a.tlen = 10000
         a.related = True
-        a.cpu_pairs = min(a.cpu_pairs, 64)
+        a.cpu_pairs = min(a.cpu_pairs, 64 if a.gap_open is None else 32)
     return a
 
 
 MODES = {"global": 0, "local": 1, "semiGlobal": 2}
 
 
-def fill_alg_bytes(batch, cigar: bool) -> int:
+def fill_alg_bytes(batch, cigar: bool, affine: bool = False) -> int:
     """Algorithmic HBM bytes of one fill launch: the sequence
-    bytes read, the 2-bit traceback code per DP cell written (cigar on) and
-    16 B of per-pair results (score, target_begin, goal cell)."""
+    bytes read, the 2-bit (affine: 4-bit) traceback code per DP cell written
+    (cigar on) and 16 B of per-pair results (score, target_begin, goal cell)."""
     n = batch.qlen.astype(np.int64)
     m = batch.tlen.astype(np.int64)
     b = n + m + 16
     if cigar:
-        b = b + (n * m + 3) // 4
+        b = b + ((n * m + 1) // 2 if affine else (n * m + 3) // 4)
     return int(b.sum())
 
 
-def cpu_baseline(batch, mode, sc, cigar, pairs, threads):
+def cpu_baseline(batch, mode, sc, cigar, pairs, threads, gap_open=None):
     from oracle.pyoracle import Oracle, Reference
 
-    impl = Reference() if Reference.available() else Oracle()
+    affine = gap_open is not None
+    impl = Reference() if Reference.available() and not affine else Oracle()
     sample = batch.slice(0, min(pairs, batch.n_pairs))
     t0 = time.perf_counter()
-    res = impl.align_batch(sample, mode, *sc, cigar, n_threads=threads)
+    if affine:  # the reference has no affine Align: the CPU definition (oracle/affine_oracle.c) is the baseline
+        res = impl.align_affine_batch(sample, mode, sc[0], sc[1], gap_open, sc[2], cigar, n_threads=threads)
+    else:
+        res = impl.align_batch(sample, mode, *sc, cigar, n_threads=threads)
     dt = time.perf_counter() - t0
     assert not res.status.any()
     return {"value": round(sample.cells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": impl.kind,
             "sample": f"first {sample.n_pairs} pairs of the same batch ({sample.cells:.3g} cells), "
                       f"OpenMP over pairs, {dt:.2f} s wall",
             "impl": "oracle/_ref/libref_align.so (reference team_alignment.cpp, g++ -O3)" if impl.kind == "reference"
-            else "oracle/liboracle.so (C restatement)"}
+            else ("oracle/liboracle.so (affine_oracle.c: the extension's CPU definition)" if affine
+                  else "oracle/liboracle.so (C restatement)")}
+
+
+def parity_vs_oracle(res, batch, mode, sc, gap_open, k):
+    """Affine extension (no reference digest exists for gap_open != 0): the
+    first k pairs against the CPU definition (oracle/affine_oracle.c)."""
+    from oracle.pyoracle import Oracle
+
+    sub = batch.slice(0, min(k, batch.n_pairs))
+    want = Oracle().align_affine_batch(sub, mode, sc[0], sc[1], gap_open, sc[2], res.cigar_lens is not None)
+    ok = bool(np.array_equal(res.scores[: sub.n_pairs], want.scores)
+              and np.array_equal(res.target_begins[: sub.n_pairs], want.target_begins))
+    if res.cigar_lens is not None:
+        ok = ok and all(res.cigar(p) == want.cigar(p) for p in range(sub.n_pairs))
+    return {"oracle": "oracle/affine_oracle.c (definition; parity vs the reference unpinned for gap_open != 0)",
+            "pairs_checked": sub.n_pairs, "bit_exact": ok}
 
 
 def parity_vs_digest(res, batch, args):
@@ -135,7 +158,7 @@ def parity_vs_digest(res, batch, args):
         name, k = "cfg3_semi_sample", 64
     elif args.workload == "cfg5" and (args.mode, args.scoring) == ("semiGlobal", "1,-1,-1") and batch.n_pairs >= 32:
         name, k = "cfg5_semi_sample", 32
-    if name is None or res.cigar_lens is None:
+    if name is None or res.cigar_lens is None or (args.gap_open or 0) != 0:
         return None
     import hashlib
 
@@ -159,7 +182,8 @@ def workload_name(args, cigar):
         return (f"config 3 stand-in: {args.pairs} ONT-like reads per GPU (log-normal 1-20 kb, median 9 kb, 10% error, "
                 f"50% reverse) of a 4.64 Mb synthetic genome vs their true-origin windows, {tail}")
     pre = {"cfg2": "config 2: " if (args.qlen, args.tlen, args.pairs) == (1000, 1000, 10000) else "",
-           "cfg5": "config 5 sample (linear gap): "}[args.workload]
+           "cfg5": ("config 5 sample (linear gap): " if args.gap_open is None else
+                    f"config 5 sample, affine gaps (open {args.gap_open}, extend {args.scoring.split(',')[2]}): ")}[args.workload]
     return pre + (f"{args.pairs} {'related' if args.related else 'uniform'} {args.qlen}x{args.tlen} pairs per GPU, "
                   f"{tail}")
 
@@ -337,7 +361,8 @@ def main():
         batch = gen(P, args.qlen, args.tlen, 0x5EED, first_pair=rank * P)
 
     al = Aligner(dev_index)
-    plan = DevicePlan(al, batch, mode, *sc, cigar, workspace_budget=int(args.workspace_gb * 2**30))
+    plan = DevicePlan(al, batch, mode, *sc, cigar, workspace_budget=int(args.workspace_gb * 2**30),
+                      gap_open=args.gap_open)
     stream = torch.cuda.current_stream(dev)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo: host tensors
     rec = torch.zeros((3, P), dtype=torch.int32, device=coll_dev)
@@ -358,6 +383,8 @@ def main():
         if args.warmup == 0:
             step()
         parity = parity_vs_digest(plan.results(), batch, args)
+        if parity is None and args.gap_open is not None:
+            parity = parity_vs_oracle(plan.results(), batch, mode, sc, args.gap_open, 16)
 
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -399,14 +426,17 @@ def main():
             kt.append(f_ms)
             tt.append(t_ms)
         fill_ms = float(np.mean(kt))
-        alg = fill_alg_bytes(batch, cigar)
+        alg = fill_alg_bytes(batch, cigar, args.gap_open is not None)
         achieved = alg / (fill_ms / 1e3) / 1e9 if alg else None
         tag = (f"{args.mode}_{'cigar' if cigar else 'score'}_{args.pairs}x{args.qlen}x{args.tlen}" if args.workload != "cfg3"
                else f"cfg3_{'cigar' if cigar else 'score'}_{args.pairs}")
+        if args.gap_open is not None:
+            tag = "affine_" + tag
         traffic = load_traffic(tag)
         roof = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": traffic, "kernel": "fill_kernel", "kernel_ms": round(fill_ms, 4),
+                "traffic": traffic, "kernel": "affine_fill_kernel" if args.gap_open is not None else "fill_kernel",
+                "kernel_ms": round(fill_ms, 4),
                 "alg_bytes_per_launch": alg,
                 "note": "integer DP: VALU-bound, not HBM- or MFMA-bound (see valu)"}
         ops_per_cell = None
@@ -421,7 +451,7 @@ def main():
         cpu = None
         if world == 1 and not args.no_cpu:
             thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(batch, mode, sc, cigar, args.cpu_pairs, thr)
+            cpu = cpu_baseline(batch, mode, sc, cigar, args.cpu_pairs, thr, args.gap_open)
         out = {
             "metric": "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; bit-exact score+CIGAR",
             "value": round(gcups, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,

@@ -26,7 +26,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libteam_alignment.so")
 
-TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY = range(6)
+TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY, TA_ERR_RANGE = range(7)
 
 
 class AlignmentType(enum.IntEnum):
@@ -87,6 +87,22 @@ def lib() -> C.CDLL:
     L.ta_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ta_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     L.ta_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+    # affine-gap extension (include/team_align_c.h, no reference counterpart)
+    L.ta_align_batch_affine.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, u64p, u32p, C.c_void_p, u64p, u32p,
+                                        C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p, u32p, C.c_void_p,
+                                        C.c_uint64, u64p, u32p]
+    L.ta_affine_plan_create.argtypes = [C.c_void_p, C.c_uint32, u32p, u32p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                        C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_void_p)]
+    L.ta_affine_plan_destroy.argtypes = [C.c_void_p]
+    L.ta_affine_plan_destroy.restype = None
+    for f in ("ta_affine_plan_cigar_slots_bytes", "ta_affine_plan_workspace_bytes"):
+        getattr(L, f).restype = C.c_uint64
+        getattr(L, f).argtypes = [C.c_void_p]
+    L.ta_affine_plan_chunks.restype = C.c_uint32
+    L.ta_affine_plan_chunks.argtypes = [C.c_void_p]
+    L.ta_affine_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ta_affine_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+    L.ta_affine_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     _lib = L
     return L
 
@@ -96,6 +112,9 @@ ABI_SYMBOLS = [
     "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_cigar_slot_bytes",
     "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes",
     "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_execute", "ta_plan_execute_fill", "ta_plan_execute_traceback",
+    "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
+    "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
+    "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
 ]
 # The drop-in C++ entry point (team_alignment.hpp), g++/libstdc++ cxx11 mangling.
 TEAM_ALIGN_SYMBOL = ("_ZN4team5AlignEPKcjS1_jNS_13AlignmentTypeEiiiPNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEEPj")
@@ -111,7 +130,7 @@ def _check_type(type) -> int:
 def _raise(status: int, ctx=None):
     L = lib()
     msg = L.ta_status_string(status).decode()
-    if status in (TA_ERR_BAD_TYPE, TA_ERR_CIGAR):
+    if status in (TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_RANGE):
         raise ValueError(msg)
     detail = L.ta_last_error(ctx).decode() if ctx else ""
     raise DeviceError(f"{msg}: {detail}" if detail else msg)
@@ -168,6 +187,16 @@ class Aligner:
 
     def align_batch(self, batch, type, match: int, mismatch: int, gap: int, want_cigar: bool = True) -> BatchResult:
         """Batched team::Align over a bioinfo1_amd.synth.PairBatch."""
+        return self._batch(batch, type, (match, mismatch, gap), want_cigar, affine=False)
+
+    def align_batch_affine(self, batch, type, match: int, mismatch: int, gap_open: int, gap_extend: int,
+                           want_cigar: bool = True) -> BatchResult:
+        """The affine-gap extension (ta_align_batch_affine): a gap of length L costs
+        gap_open + L*gap_extend.  No reference counterpart; gap_open == 0 gives
+        exactly team::Align with gap = gap_extend."""
+        return self._batch(batch, type, (match, mismatch, gap_open, gap_extend), want_cigar, affine=True)
+
+    def _batch(self, batch, type, scoring, want_cigar, affine) -> BatchResult:
         L = lib()
         t = _check_type(type)
         P = batch.n_pairs
@@ -182,9 +211,10 @@ class Aligner:
             clen = np.zeros(P, np.uint32)
         qb = batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8)
         tbb = batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8)
-        r = L.ta_align_batch(
+        fn = L.ta_align_batch_affine if affine else L.ta_align_batch
+        r = fn(
             self._h, P, qb.ctypes.data, _p(batch.qoff, C.c_uint64), _p(batch.qlen, C.c_uint32), tbb.ctypes.data,
-            _p(batch.toff, C.c_uint64), _p(batch.tlen, C.c_uint32), t, match, mismatch, gap, int(bool(want_cigar)),
+            _p(batch.toff, C.c_uint64), _p(batch.tlen, C.c_uint32), t, *scoring, int(bool(want_cigar)),
             _p(sc, C.c_int32), _p(tb, C.c_uint32), arena.ctypes.data if want_cigar else None, cap,
             _p(coff, C.c_uint64) if want_cigar else None, _p(clen, C.c_uint32) if want_cigar else None)
         if r != TA_OK:
@@ -212,6 +242,17 @@ def align(query: bytes, target: bytes, type, match: int, mismatch: int, gap: int
     return int(res.scores[0]), res.cigar(0), int(res.target_begins[0])
 
 
+def align_affine(query: bytes, target: bytes, type, match: int, mismatch: int, gap_open: int, gap_extend: int,
+                 want_cigar: bool = True):
+    """The affine-gap extension for one pair -> (score, cigar bytes or None, target_begin)."""
+    from .synth import from_pairs
+
+    _check_type(type)
+    res = default_aligner().align_batch_affine(from_pairs([(bytes(query), bytes(target))]), type, match, mismatch,
+                                               gap_open, gap_extend, want_cigar)
+    return int(res.scores[0]), res.cigar(0), int(res.target_begins[0])
+
+
 class _DeviceIO(C.Structure):
     _fields_ = [("query_bytes", C.c_void_p), ("query_off", C.c_void_p), ("target_bytes", C.c_void_p),
                 ("target_off", C.c_void_p), ("score", C.c_void_p), ("target_begin", C.c_void_p),
@@ -226,7 +267,9 @@ class DevicePlan:
     current torch stream (asynchronous)."""
 
     def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, device=None,
-                 workspace_budget: int = 0):
+                 workspace_budget: int = 0, gap_open=None):
+        """gap_open=None: team::Align's linear gap.  gap_open=o: the affine-gap
+        extension (ta_affine_plan_*) with gap_extend = gap."""
         import torch
 
         L = lib()
@@ -235,9 +278,14 @@ class DevicePlan:
         self.dev = torch.device("cuda", aligner.device) if device is None else device
         self.P = batch.n_pairs
         self.want_cigar = bool(want_cigar)
+        self.affine = gap_open is not None
+        self._fn = (lambda name: getattr(L, name.replace("ta_plan_", "ta_affine_plan_"))) if self.affine else \
+            (lambda name: getattr(L, name))
         h = C.c_void_p()
-        r = L.ta_plan_create(aligner.handle, self.P, _p(batch.qlen, C.c_uint32), _p(batch.tlen, C.c_uint32), t,
-                             match, mismatch, gap, int(self.want_cigar), workspace_budget, C.byref(h))
+        scoring = (match, mismatch, gap_open, gap) if self.affine else (match, mismatch, gap)
+        r = self._fn("ta_plan_create")(aligner.handle, self.P, _p(batch.qlen, C.c_uint32),
+                                       _p(batch.tlen, C.c_uint32), t, *scoring, int(self.want_cigar),
+                                       workspace_budget, C.byref(h))
         if r != TA_OK:
             _raise(r, aligner.handle)
         self._h = h
@@ -249,7 +297,7 @@ class DevicePlan:
         self.toff = f(batch.toff.view(np.int64))
         self.score = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
         self.target_begin = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
-        self.slots_bytes = int(L.ta_plan_cigar_slots_bytes(h))
+        self.slots_bytes = int(self._fn("ta_plan_cigar_slots_bytes")(h))
         self.slots = torch.zeros(max(self.slots_bytes, 1) if self.want_cigar else 1, dtype=torch.uint8,
                                  device=self.dev)
         self.cigar_start = torch.zeros(self.P, dtype=torch.int64, device=self.dev)
@@ -257,26 +305,26 @@ class DevicePlan:
         self.io = _DeviceIO(self.qbytes.data_ptr(), self.qoff.data_ptr(), self.tbytes.data_ptr(),
                             self.toff.data_ptr(), self.score.data_ptr(), self.target_begin.data_ptr(),
                             self.slots.data_ptr(), self.cigar_start.data_ptr(), self.cigar_len.data_ptr())
-        self.workspace_bytes = int(L.ta_plan_workspace_bytes(h))
-        self.chunks = int(L.ta_plan_chunks(h))
-        self.dual_pairs = int(L.ta_plan_dual_pairs(h))
-        self.flex_pairs = int(L.ta_plan_flex_pairs(h))
+        self.workspace_bytes = int(self._fn("ta_plan_workspace_bytes")(h))
+        self.chunks = int(self._fn("ta_plan_chunks")(h))
+        self.dual_pairs = 0 if self.affine else int(L.ta_plan_dual_pairs(h))
+        self.flex_pairs = 0 if self.affine else int(L.ta_plan_flex_pairs(h))
 
     def _stream(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
 
     def run(self):
-        r = lib().ta_plan_execute(self._h, C.byref(self.io), self._stream())
+        r = self._fn("ta_plan_execute")(self._h, C.byref(self.io), self._stream())
         if r != TA_OK:
             _raise(r, self._ctx)
 
     def run_fill(self, chunk: int = 0):
-        r = lib().ta_plan_execute_fill(self._h, C.byref(self.io), self._stream(), chunk)
+        r = self._fn("ta_plan_execute_fill")(self._h, C.byref(self.io), self._stream(), chunk)
         if r != TA_OK:
             _raise(r, self._ctx)
 
     def run_traceback(self, chunk: int = 0):
-        r = lib().ta_plan_execute_traceback(self._h, C.byref(self.io), self._stream(), chunk)
+        r = self._fn("ta_plan_execute_traceback")(self._h, C.byref(self.io), self._stream(), chunk)
         if r != TA_OK:
             _raise(r, self._ctx)
 
@@ -294,7 +342,7 @@ class DevicePlan:
 
     def close(self):
         if getattr(self, "_h", None):
-            lib().ta_plan_destroy(self._h)
+            self._fn("ta_plan_destroy")(self._h)
             self._h = None
 
     def __del__(self):

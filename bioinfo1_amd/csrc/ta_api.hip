@@ -13,33 +13,8 @@
 #include <vector>
 
 #include "../../include/team_align_c.h"
+#include "ta_context.h"
 #include "ta_internal.h"
-
-struct ta_context {
-    int device = 0;
-    hipStream_t stream = nullptr;
-    // a second stream on which a chunk's int32 fill (single pairs) runs beside
-    // its packed two-pair fill; the caller's stream waits for it (fork / join)
-    hipStream_t aux = nullptr, aux2 = nullptr;  // aux2: the equal-shape dual fill beside the flexible one
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join2 = nullptr;
-    // staged plans: tracebacks on their own stream, one event per stage
-    hipStream_t tbs = nullptr;
-    hipEvent_t ev_tb_done = nullptr;
-    std::vector<hipEvent_t> ev_stage;
-    std::string last_error;
-    std::mutex mu;  // one batch at a time per context
-    // grow-only device staging for ta_align_batch
-    struct Buf {
-        void* p = nullptr;
-        size_t cap = 0;
-    };
-    Buf qbytes, tbytes, qoff, toff, score, tb, slots, cstart, clen, dst_off, dst;
-    // Traceback-code and pass-boundary workspace, shared by every plan of this
-    // context and grown at execute time (a plan's chunks are sized by its
-    // budget): plans of one context must not execute concurrently.
-    Buf ws_ptrs, ws_bnd;
-    uint32_t epoch = 0;  // flexible-fill launches so far (tags of their pass hand-off records)
-};
 
 struct ta_plan {
     ta_context* ctx = nullptr;
@@ -137,6 +112,7 @@ const char* ta_status_string(int status) {
         case TA_ERR_ARG: return "invalid argument";
         case TA_ERR_DEVICE: return "device error";
         case TA_ERR_CAPACITY: return "cigar arena too small";
+        case TA_ERR_RANGE: return "affine scoring out of range";
         default: return "unknown status";
     }
 }
@@ -604,27 +580,20 @@ int ta_plan_execute_traceback(ta_plan* pl, const ta_device_io* io, void* stream,
     return exec_chunk(pl, io, s, chunk, false, true);
 }
 
-int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff, const uint32_t* qlen,
-                   const char* tbytes, const uint64_t* toff, const uint32_t* tlen, int type, int match,
-                   int mismatch, int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* arena,
-                   uint64_t arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len) {
-    if (!ctx) return TA_ERR_ARG;
-    if (!valid_type(type)) return fail(ctx, TA_ERR_BAD_TYPE, ta_status_string(TA_ERR_BAD_TYPE));
-    if (n_pairs == 0) return TA_OK;
-    if (!qoff || !qlen || !toff || !tlen) return fail(ctx, TA_ERR_ARG, "null input array");
-    if (want_cigar && (!arena || !cigar_off || !cigar_len)) return fail(ctx, TA_ERR_ARG, "null cigar output");
-    std::lock_guard<std::mutex> lock(ctx->mu);
-    TA_HIP(ctx, hipSetDevice(ctx->device));
+}  // extern "C"
+
+namespace {
+
+// The host-memory batch around a device plan (linear or affine): stage the
+// inputs in the context's grow-only buffers, run `exec`, bring back scores,
+// target_begins and the compacted CIGARs.  `slots_bytes` is the plan's CIGAR
+// slot arena.  Called with ctx->mu held.
+template <class Exec>
+int host_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff, const uint32_t* qlen,
+               const char* tbytes, const uint64_t* toff, const uint32_t* tlen, uint64_t qend, uint64_t tend,
+               int want_cigar, int32_t* score, uint32_t* target_begin, char* arena, uint64_t arena_bytes,
+               uint64_t* cigar_off, uint32_t* cigar_len, uint64_t slots_bytes, Exec&& exec) {
     hipStream_t s = ctx->stream;
-    // input extents
-    uint64_t qend = 0, tend = 0;
-    for (uint32_t p = 0; p < n_pairs; ++p) {
-        qend = std::max<uint64_t>(qend, qoff[p] + qlen[p]);
-        tend = std::max<uint64_t>(tend, toff[p] + tlen[p]);
-    }
-    if ((qend && !qb) || (tend && !tbytes)) return fail(ctx, TA_ERR_ARG, "null sequence bytes");
-    ta_plan* pl = nullptr;
-    if (int r = ta_plan_create(ctx, n_pairs, qlen, tlen, type, match, mismatch, gap, want_cigar, 0, &pl)) return r;
     int rc = TA_OK;
     auto chk = [&](int r) {
         if (r != TA_OK && rc == TA_OK) rc = r;
@@ -634,7 +603,7 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
     if (chk(grow(ctx, ctx->qbytes, qend)) && chk(grow(ctx, ctx->tbytes, tend)) &&
         chk(grow(ctx, ctx->qoff, P * 8)) && chk(grow(ctx, ctx->toff, P * 8)) && chk(grow(ctx, ctx->score, P * 4)) &&
         chk(grow(ctx, ctx->tb, P * 4)) &&
-        (!want_cigar || (chk(grow(ctx, ctx->slots, pl->slots_bytes)) && chk(grow(ctx, ctx->cstart, P * 8)) &&
+        (!want_cigar || (chk(grow(ctx, ctx->slots, slots_bytes)) && chk(grow(ctx, ctx->cstart, P * 8)) &&
                          chk(grow(ctx, ctx->clen, P * 4)) && chk(grow(ctx, ctx->dst_off, P * 8))))) {
         auto cp = [&](void* d, const void* h, size_t b) {
             if (!b || rc != TA_OK) return;
@@ -655,7 +624,7 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
         io.cigar_slots = (char*)ctx->slots.p;
         io.cigar_start = (uint64_t*)ctx->cstart.p;
         io.cigar_len = (uint32_t*)ctx->clen.p;
-        if (rc == TA_OK) chk(ta_plan_execute(pl, &io, s));
+        if (rc == TA_OK) chk(exec(&io, s));
         std::vector<int32_t> sc(P);
         std::vector<uint32_t> tb(P);
         auto dn = [&](void* h, const void* d, size_t b) {
@@ -703,7 +672,73 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
             if (target_begin) std::memcpy(target_begin, tb.data(), P * 4);
         }
     }
+    return rc;
+}
+
+// Argument checks shared by the two host-memory batch entries; sets the input extents.
+int check_host_batch(ta_context* ctx, int type, uint32_t n_pairs, const char* qb, const uint64_t* qoff,
+                     const uint32_t* qlen, const char* tbytes, const uint64_t* toff, const uint32_t* tlen,
+                     int want_cigar, char* arena, uint64_t* cigar_off, uint32_t* cigar_len, uint64_t* qend,
+                     uint64_t* tend) {
+    if (!ctx) return TA_ERR_ARG;
+    if (!valid_type(type)) return fail(ctx, TA_ERR_BAD_TYPE, ta_status_string(TA_ERR_BAD_TYPE));
+    if (n_pairs == 0) return TA_OK;
+    if (!qoff || !qlen || !toff || !tlen) return fail(ctx, TA_ERR_ARG, "null input array");
+    if (want_cigar && (!arena || !cigar_off || !cigar_len)) return fail(ctx, TA_ERR_ARG, "null cigar output");
+    *qend = *tend = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        *qend = std::max<uint64_t>(*qend, qoff[p] + qlen[p]);
+        *tend = std::max<uint64_t>(*tend, toff[p] + tlen[p]);
+    }
+    if ((*qend && !qb) || (*tend && !tbytes)) return fail(ctx, TA_ERR_ARG, "null sequence bytes");
+    return TA_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff, const uint32_t* qlen,
+                   const char* tbytes, const uint64_t* toff, const uint32_t* tlen, int type, int match,
+                   int mismatch, int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* arena,
+                   uint64_t arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len) {
+    uint64_t qend = 0, tend = 0;
+    if (int r = check_host_batch(ctx, type, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, want_cigar, arena,
+                                 cigar_off, cigar_len, &qend, &tend))
+        return r;
+    if (n_pairs == 0) return TA_OK;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    ta_plan* pl = nullptr;
+    if (int r = ta_plan_create(ctx, n_pairs, qlen, tlen, type, match, mismatch, gap, want_cigar, 0, &pl)) return r;
+    const int rc = host_batch(ctx, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, qend, tend, want_cigar, score,
+                              target_begin, arena, arena_bytes, cigar_off, cigar_len, pl->slots_bytes,
+                              [&](const ta_device_io* io, hipStream_t s) { return ta_plan_execute(pl, io, s); });
     ta_plan_destroy(pl);
+    return rc;
+}
+
+int ta_align_batch_affine(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff,
+                          const uint32_t* qlen, const char* tbytes, const uint64_t* toff, const uint32_t* tlen,
+                          int type, int match, int mismatch, int gap_open, int gap_extend, int want_cigar,
+                          int32_t* score, uint32_t* target_begin, char* arena, uint64_t arena_bytes,
+                          uint64_t* cigar_off, uint32_t* cigar_len) {
+    uint64_t qend = 0, tend = 0;
+    if (int r = check_host_batch(ctx, type, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, want_cigar, arena,
+                                 cigar_off, cigar_len, &qend, &tend))
+        return r;
+    if (n_pairs == 0) return TA_OK;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    ta_affine_plan* pl = nullptr;
+    if (int r = ta_affine_plan_create(ctx, n_pairs, qlen, tlen, type, match, mismatch, gap_open, gap_extend,
+                                      want_cigar, 0, &pl))
+        return r;
+    const int rc = host_batch(ctx, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, qend, tend, want_cigar, score,
+                              target_begin, arena, arena_bytes, cigar_off, cigar_len,
+                              ta_affine_plan_cigar_slots_bytes(pl),
+                              [&](const ta_device_io* io, hipStream_t s) { return ta_affine_plan_execute(pl, io, s); });
+    ta_affine_plan_destroy(pl);
     return rc;
 }
 

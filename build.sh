@@ -25,6 +25,8 @@ for m in 0 2; do
   done
 done
 "$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$CS/ta_kernels.hip" -o "$B/ta_misc.o" & pids+=($!)
+# affine-gap extension (fill + traceback kernels and its plan driver)
+"$HIPCC" "${FLAGS[@]}" -c "$CS/ta_affine.hip" -o "$B/ta_affine.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip" -o "$B/ta_api.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp" -o "$B/shim.o" & pids+=($!)
 # mapper stages (libteam_mapper.so) and the team_mapper_amd CLI
@@ -36,7 +38,7 @@ for f in tm_api tm_fastx; do
 done
 "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp" -o "$B/tm_main.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,2}{0,1}.o "$B/ta_misc.o" "$B/ta_api.o" "$B/shim.o" -o "$OUT"
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/shim.o" -o "$OUT"
 PKG="$ROOT/bioinfo1_amd"
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/tm_{minimizers,match,chain,api,fastx}.o -L"$PKG" -lteam_alignment -lz \
   -Wl,-rpath,'$ORIGIN' -o "$PKG/libteam_mapper.so"

@@ -124,6 +124,46 @@ int ta_plan_execute(ta_plan* plan, const ta_device_io* io, void* hip_stream);
 int ta_plan_execute_fill(ta_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
 int ta_plan_execute_traceback(ta_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
 
+/*
+ * ---- Affine-gap extension (BASELINE config 5: "affine gaps + full CIGAR
+ * traceback").  The reference has NO counterpart: team::Align is linear-gap
+ * only (team_alignment.cpp:25-28, 102-116; the "Gotoh" of
+ * team_alignment.hpp:11 is a label).  The semantics are defined in
+ * oracle/affine_oracle.c (Gotoh E/F/H, the reference's tie order, boundaries,
+ * goals, traceback and CIGAR format); a gap of length L costs
+ * gap_open + L * gap_extend and a '-' byte makes its gap step free.  With
+ * gap_open == 0 the results are byte-identical to team::Align with
+ * gap = gap_extend (that part of parity is pinned to the reference goldens;
+ * gap_open != 0 is unpinned).
+ * Range: (max qlen + max tlen + 2) * max(|match|, |mismatch|,
+ * |gap_open| + |gap_extend|) must be < 2^26, else TA_ERR_RANGE.
+ */
+#define TA_ERR_RANGE 6 /* affine scoring x lengths outside the int32-safe range */
+
+typedef struct ta_affine_plan ta_affine_plan;
+
+/* As ta_plan_create, with the affine scoring.  Traceback codes take 4 bits per
+ * cell (source M/I/D/STOP + the E and F extension bits). */
+int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
+                          const uint32_t* target_len_host, int type, int match, int mismatch, int gap_open,
+                          int gap_extend, int want_cigar, uint64_t workspace_budget, ta_affine_plan** out);
+void ta_affine_plan_destroy(ta_affine_plan* plan);
+uint64_t ta_affine_plan_cigar_slots_bytes(const ta_affine_plan* plan);
+uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* plan);
+uint32_t ta_affine_plan_chunks(const ta_affine_plan* plan);
+/* Enqueue the whole batch / one chunk's fill / one chunk's traceback on hip_stream. */
+int ta_affine_plan_execute(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream);
+int ta_affine_plan_execute_fill(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
+int ta_affine_plan_execute_traceback(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream,
+                                     uint32_t chunk);
+
+/* Host-memory batch with affine gaps: ta_align_batch with gap -> (gap_open, gap_extend). */
+int ta_align_batch_affine(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, const uint64_t* query_off,
+                          const uint32_t* query_len, const char* target_bytes, const uint64_t* target_off,
+                          const uint32_t* target_len, int type, int match, int mismatch, int gap_open,
+                          int gap_extend, int want_cigar, int32_t* score, uint32_t* target_begin,
+                          char* cigar_arena, uint64_t cigar_arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len);
+
 #ifdef __cplusplus
 }
 #endif

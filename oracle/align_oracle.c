@@ -88,6 +88,11 @@ static int or_rle(const char* ops, size_t len, char* out, size_t cap, size_t* ou
     return OR_OK;
 }
 
+/* The same RLE for affine_oracle.c (the extension shares the reference's CIGAR format). */
+int or_rle_public(const char* ops, size_t len, char* out, size_t cap, size_t* out_len) {
+    return or_rle(ops, len, out, cap, out_len);
+}
+
 /*
  * oracle_align -- restates team::Align (team_alignment.cpp:49-350).
  *   type: 0 global, 1 local, 2 semiGlobal (team_alignment.hpp:8-12).

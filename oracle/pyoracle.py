@@ -1,6 +1,8 @@
 """ctypes bindings for the CPU checkers (TEST INFRASTRUCTURE ONLY).
 
-* ``Oracle``    -- oracle/liboracle.so, our C restatement (align_oracle.c)
+* ``Oracle``    -- oracle/liboracle.so, our C restatement (align_oracle.c),
+                   plus the affine-gap extension's definition (affine_oracle.c;
+                   ``align_affine*``, parity unpinned for gap_open != 0)
 * ``Reference`` -- oracle/_ref/libref_align.so, the unmodified reference
                    team_alignment.cpp compiled by oracle/Makefile (present
                    only where it was built; it is never committed).
@@ -20,7 +22,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "liboracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libref_align.so")
 
-ERR_MSG = {1: "Unknown AlignmentType provided.", 2: "Unknown error in determining cigar string."}
+ERR_MSG = {1: "Unknown AlignmentType provided.", 2: "Unknown error in determining cigar string.",
+           5: "affine scoring out of range"}
 
 
 class AlignError(ValueError):
@@ -62,6 +65,11 @@ class Oracle(_Base):
                                      C.c_size_t, C.POINTER(C.c_size_t)]
         lib.oracle_align_batch.restype = C.c_int
         lib.oracle_max_threads.restype = C.c_int
+        lib.oracle_align_affine.restype = C.c_int
+        lib.oracle_align_affine.argtypes = [C.c_char_p, C.c_uint, C.c_char_p, C.c_uint, C.c_int, C.c_int, C.c_int,
+                                            C.c_int, C.c_int, C.c_int, C.POINTER(C.c_int), C.POINTER(C.c_uint),
+                                            C.c_char_p, C.c_size_t, C.POINTER(C.c_size_t)]
+        lib.oracle_align_affine_batch.restype = C.c_int
         self.lib = lib
 
     def max_threads(self) -> int:
@@ -90,6 +98,37 @@ class Oracle(_Base):
             C.c_int(int(type)), C.c_int(match), C.c_int(mismatch), C.c_int(gap), C.c_int(int(bool(want_cigar))),
             C.c_int(n_threads), _ptr(sc, C.c_int32), _ptr(tb, C.c_uint32), _ptr(arena, C.c_char),
             _ptr(off, C.c_uint64), _ptr(cl, C.c_uint32), _ptr(st, C.c_int32))
+        return BatchResult(sc, tb, cl, st, arena, off, want_cigar)
+
+
+    def align_affine(self, q: bytes, t: bytes, type: int, match: int, mismatch: int, gap_open: int, gap_extend: int,
+                     want_cigar=True):
+        cap = cigar_bound(len(q), len(t))
+        buf = C.create_string_buffer(cap)
+        sc, tb, cl = C.c_int(0), C.c_uint(0), C.c_size_t(0)
+        r = self.lib.oracle_align_affine(q, len(q), t, len(t), int(type), match, mismatch, gap_open, gap_extend,
+                                         int(bool(want_cigar)), C.byref(sc), C.byref(tb), buf, C.c_size_t(cap),
+                                         C.byref(cl))
+        if r:
+            raise AlignError(ERR_MSG.get(r, f"oracle status {r}"))
+        return sc.value, (buf.raw[: cl.value] if want_cigar else None), tb.value
+
+    def affine_in_range(self, n, m, match, mismatch, gap_open, gap_extend) -> bool:
+        return bool(self.lib.oracle_affine_in_range(C.c_uint(n), C.c_uint(m), match, mismatch, gap_open, gap_extend))
+
+    def align_affine_batch(self, batch, type, match, mismatch, gap_open, gap_extend, want_cigar=True, n_threads=0):
+        P = batch.n_pairs
+        off, cap, arena = self._slots(batch)
+        sc = np.zeros(P, np.int32)
+        tb = np.zeros(P, np.uint32)
+        cl = np.zeros(P, np.uint32)
+        st = np.zeros(P, np.int32)
+        self.lib.oracle_align_affine_batch(
+            C.c_uint(P), _ptr(batch.qbytes, C.c_char), _ptr(batch.qoff, C.c_uint64), _ptr(batch.qlen, C.c_uint32),
+            _ptr(batch.tbytes, C.c_char), _ptr(batch.toff, C.c_uint64), _ptr(batch.tlen, C.c_uint32),
+            C.c_int(int(type)), C.c_int(match), C.c_int(mismatch), C.c_int(gap_open), C.c_int(gap_extend),
+            C.c_int(int(bool(want_cigar))), C.c_int(n_threads), _ptr(sc, C.c_int32), _ptr(tb, C.c_uint32),
+            _ptr(arena, C.c_char), _ptr(off, C.c_uint64), _ptr(cl, C.c_uint32), _ptr(st, C.c_int32))
         return BatchResult(sc, tb, cl, st, arena, off, want_cigar)
 
 
@@ -166,4 +205,26 @@ def cigar_check_batch(batch, type, match, mismatch, gap, scores, target_begins, 
         _ptr(batch.tbytes, C.c_char), _ptr(batch.toff, C.c_uint64), _ptr(batch.tlen, C.c_uint32),
         C.c_int(int(type)), C.c_int(match), C.c_int(mismatch), C.c_int(gap), _ptr(sc, C.c_int32),
         _ptr(tb, C.c_uint32), _ptr(ar, C.c_char), _ptr(co, C.c_uint64), _ptr(cl, C.c_uint32), _ptr(st, C.c_int32))
+    return st
+
+
+def affine_cigar_check_batch(batch, type, match, mismatch, gap_open, gap_extend, scores, target_begins, arena,
+                             cigar_off, cigar_len):
+    """Affine-extension analogue of cigar_check_batch (oracle_affine_cigar_check;
+    exact for gap_open <= 0): per-pair status, 0 = consistent."""
+    build()
+    lib = C.CDLL(ORACLE_SO)
+    P = batch.n_pairs
+    st = np.zeros(P, np.int32)
+    sc = np.ascontiguousarray(scores, dtype=np.int32)
+    tb = np.ascontiguousarray(target_begins, dtype=np.uint32)
+    co = np.ascontiguousarray(cigar_off, dtype=np.uint64)
+    cl = np.ascontiguousarray(cigar_len, dtype=np.uint32)
+    ar = np.ascontiguousarray(arena, dtype=np.uint8)
+    lib.oracle_affine_cigar_check_batch(
+        C.c_uint(P), _ptr(batch.qbytes, C.c_char), _ptr(batch.qoff, C.c_uint64), _ptr(batch.qlen, C.c_uint32),
+        _ptr(batch.tbytes, C.c_char), _ptr(batch.toff, C.c_uint64), _ptr(batch.tlen, C.c_uint32),
+        C.c_int(int(type)), C.c_int(match), C.c_int(mismatch), C.c_int(gap_open), C.c_int(gap_extend),
+        _ptr(sc, C.c_int32), _ptr(tb, C.c_uint32), _ptr(ar, C.c_char), _ptr(co, C.c_uint64), _ptr(cl, C.c_uint32),
+        _ptr(st, C.c_int32))
     return st
