@@ -8,7 +8,11 @@ resident in HBM before the timed region, results (score, target_begin,
 CIGAR) left in HBM.  With N GPUs (torch.distributed.run, one process per
 GPU, RCCL) every rank aligns its own 10,000 pairs (weak scaling: pairs are
 independent, the batch is range-split by pair index) and the fixed-size
-per-pair records are all-gathered over RCCL inside each step.
+per-pair records of every step are all-gathered over RCCL inside the timed
+region.  --pipeline runs the K steps as one pipelined sequence of K batches
+(ta_plan_execute_batches: batch k's traceback beside batch k+1's fill, each
+batch with its own outputs).  batch_latency_ms = one batch alone (fill +
+traceback kernels, HIP events).
 
 Prints ONE JSON line (rank 0).  value = whole-job GCUPS = (sum of n*m over
 all ranks' pairs) / (max over ranks of the step time).
@@ -77,6 +81,10 @@ def parse():
     ap.add_argument("--gap-open", type=int, default=None,
                     help="affine-gap extension (no reference counterpart): a gap of length L costs "
                          "gap_open + L*gap, gap = the third --scoring value (config 5's 'affine gaps')")
+    ap.add_argument("--pipeline", action="store_true",
+                    help="run the K steps as one ta_plan_execute_batches call (batch k's traceback on a "
+                         "second stream beside batch k+1's fill) instead of ta_plan_execute per step; "
+                         "measured slower on config 2 (DESIGN.md 3.8)")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal only)")
     a = ap.parse_args()
     if a.workload == "cfg2":
@@ -365,24 +373,46 @@ def main():
                       gap_open=args.gap_open)
     stream = torch.cuda.current_stream(dev)
     coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo: host tensors
-    rec = torch.zeros((3, P), dtype=torch.int32, device=coll_dev)
-    gathered = torch.zeros((world * 3, P), dtype=torch.int32, device=coll_dev) if world > 1 else None
+    # Steps = batches.  --pipeline: ta_plan_execute_batches runs batch k's
+    # traceback beside batch k+1's fill; every batch has its own output
+    # buffers, so all K results stay intact and are gathered at the end.
+    pipelined = cigar and args.gap_open is None and args.pipeline
+    n_sets = max(args.steps, args.warmup, 2)
+    outs = [plan] + [plan.output_set() for _ in range(n_sets - 1)] if pipelined else None
 
-    def step():
-        plan.run()
+    def gather(sets):
         if world > 1:  # range-split results -> every rank (RCCL all-gather over xGMI)
-            rec[0].copy_(plan.score)
-            rec[1].copy_(plan.target_begin)
-            rec[2].copy_(plan.cigar_len)
-            dist.all_gather_into_tensor(gathered, rec)
+            rec = torch.empty((len(sets), 3, P), dtype=torch.int32, device=dev)
+            for k, o in enumerate(sets):
+                rec[k, 0].copy_(o.score)
+                rec[k, 1].copy_(o.target_begin)
+                rec[k, 2].copy_(o.cigar_len if cigar else o.score)
+            rec = rec.to(coll_dev)
+            out = torch.empty((world * len(sets), 3, P), dtype=torch.int32, device=coll_dev)
+            dist.all_gather_into_tensor(out, rec)
 
-    for _ in range(args.warmup):
-        step()
+    def run_steps(k):
+        if k <= 0:
+            return
+        if pipelined:
+            plan.run_batches(outs[:k])
+            gather(outs[:k])
+        else:
+            for _ in range(k):
+                plan.run()
+                gather([plan])
+
+    run_steps(args.warmup)
     parity = None
     if rank == 0 and not args.no_parity:
-        if args.warmup == 0:
-            step()
+        if args.warmup < (2 if pipelined else 1):
+            run_steps(2 if pipelined else 1)
         parity = parity_vs_digest(plan.results(), batch, args)
+        if parity is not None and pipelined:  # batch 1 ran beside batch 0 (capped traceback grid on its own)
+            p1 = parity_vs_digest(outs[1].results(), batch, args)
+            parity["pairs_checked"] += p1["pairs_checked"]
+            parity["bit_exact"] = parity["bit_exact"] and p1["bit_exact"]
+            parity["batches_checked"] = 2
         if parity is None and args.gap_open is not None:
             parity = parity_vs_oracle(plan.results(), batch, mode, sc, args.gap_open, 16)
 
@@ -391,8 +421,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_steps(args.steps)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -463,6 +492,8 @@ def main():
                        "cigar": cigar, "cells_per_gpu": batch.cells,
                        "parallelism": f"pairs range-split over {world} GPU(s), RCCL all-gather of per-pair records"},
             "fill_ms": round(fill_ms, 4), "traceback_ms": round(float(np.mean(tt)), 4) if cigar else None,
+            "pipelined": pipelined,
+            "batch_latency_ms": round(fill_ms + (float(np.mean(tt)) if cigar else 0.0), 4),
             "chunks": plan.chunks, "workspace_gb": round(plan.workspace_bytes / 2**30, 2),
             "roofline": roof, "valu": valu, "cpu_baseline": cpu, "parity": parity,
             "device": torch.cuda.get_device_name(dev),

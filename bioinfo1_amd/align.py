@@ -85,6 +85,8 @@ def lib() -> C.CDLL:
     L.ta_plan_flex_pairs.restype = C.c_uint32
     L.ta_plan_flex_pairs.argtypes = [C.c_void_p]
     L.ta_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+    L.ta_plan_check.argtypes = [C.c_void_p]
+    L.ta_plan_execute_batches.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
     L.ta_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     L.ta_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     # affine-gap extension (include/team_align_c.h, no reference counterpart)
@@ -111,7 +113,7 @@ def lib() -> C.CDLL:
 ABI_SYMBOLS = [
     "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_cigar_slot_bytes",
     "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes",
-    "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_execute", "ta_plan_execute_fill", "ta_plan_execute_traceback",
+    "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_execute", "ta_plan_execute_batches", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_execute_traceback",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
     "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
@@ -259,6 +261,38 @@ class _DeviceIO(C.Structure):
                 ("cigar_slots", C.c_void_p), ("cigar_start", C.c_void_p), ("cigar_len", C.c_void_p)]
 
 
+def _results(o) -> BatchResult:
+    o.torch.cuda.synchronize(o.dev)
+    sc = o.score.cpu().numpy()
+    tb = o.target_begin.cpu().numpy().view(np.uint32)
+    if not o.want_cigar:
+        return BatchResult(sc, tb, None, None, None)
+    start = o.cigar_start.cpu().numpy().view(np.uint64)
+    ln = o.cigar_len.cpu().numpy().view(np.uint32)
+    slots = o.slots.cpu().numpy()
+    return BatchResult(sc, tb, start, ln, slots)
+
+
+class PlanOutputs:
+    """A second (third, ...) set of device outputs over a DevicePlan's inputs."""
+
+    def __init__(self, plan: "DevicePlan"):
+        torch = plan.torch
+        self.torch, self.dev, self.want_cigar, self.plan = torch, plan.dev, plan.want_cigar, plan
+        self.score = torch.zeros_like(plan.score)
+        self.target_begin = torch.zeros_like(plan.target_begin)
+        self.slots = torch.zeros_like(plan.slots)
+        self.cigar_start = torch.zeros_like(plan.cigar_start)
+        self.cigar_len = torch.zeros_like(plan.cigar_len)
+        self.io = _DeviceIO(plan.qbytes.data_ptr(), plan.qoff.data_ptr(), plan.tbytes.data_ptr(),
+                            plan.toff.data_ptr(), self.score.data_ptr(), self.target_begin.data_ptr(),
+                            self.slots.data_ptr(), self.cigar_start.data_ptr(), self.cigar_len.data_ptr())
+
+    def results(self) -> BatchResult:
+        self.plan.check()
+        return _results(self)
+
+
 class DevicePlan:
     """Device-resident batch: inputs and outputs are torch tensors in HBM.
 
@@ -328,17 +362,32 @@ class DevicePlan:
         if r != TA_OK:
             _raise(r, self._ctx)
 
-    def results(self) -> BatchResult:
-        """Synchronise and copy results to host (CIGARs unpacked from slots)."""
+    def output_set(self) -> "PlanOutputs":
+        """Fresh device output buffers for the plan's inputs (one per batch of run_batches)."""
+        return PlanOutputs(self)
+
+    def run_batches(self, outs):
+        """ta_plan_execute_batches: one execution per PlanOutputs in ``outs``,
+        batch k's traceback beside batch k+1's fill (linear-gap plans)."""
+        if self.affine:
+            raise NotImplementedError("run_batches: linear-gap plans only")
+        arr = (_DeviceIO * len(outs))(*[o.io for o in outs])
+        r = lib().ta_plan_execute_batches(self._h, arr, len(outs), self._stream())
+        if r != TA_OK:
+            _raise(r, self._ctx)
+
+    def check(self):
+        """ta_plan_check after synchronising: raises DeviceError if a kernel reported an internal failure."""
         self.torch.cuda.synchronize(self.dev)
-        sc = self.score.cpu().numpy()
-        tb = self.target_begin.cpu().numpy().view(np.uint32)
-        if not self.want_cigar:
-            return BatchResult(sc, tb, None, None, None)
-        start = self.cigar_start.cpu().numpy().view(np.uint64)
-        ln = self.cigar_len.cpu().numpy().view(np.uint32)
-        slots = self.slots.cpu().numpy()
-        return BatchResult(sc, tb, start, ln, slots)
+        if not self.affine:
+            r = lib().ta_plan_check(self._h)
+            if r != TA_OK:
+                _raise(r, self._ctx)
+
+    def results(self) -> BatchResult:
+        """Synchronise, check and copy results to host (CIGARs unpacked from slots)."""
+        self.check()
+        return _results(self)
 
     def close(self):
         if getattr(self, "_h", None):

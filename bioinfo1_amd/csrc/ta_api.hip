@@ -77,7 +77,7 @@ uint64_t default_budget(const ta_context* ctx) {
     if (const char* e = std::getenv("TA_WORKSPACE_BYTES")) return std::strtoull(e, nullptr, 10);
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 48ull << 30;
-    const uint64_t avail = (uint64_t)free_b + ctx->ws_ptrs.cap + ctx->ws_bnd.cap;
+    const uint64_t avail = (uint64_t)free_b + ctx->ws_ptrs.cap + ctx->ws_bnd.cap + ctx->ws_ptrs2.cap;
     return std::max<uint64_t>(avail / 100 * 85, 1ull << 30);
 }
 
@@ -131,6 +131,7 @@ int ta_context_create(int device, ta_context** out) {
     if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return TA_ERR_DEVICE;  // kernels are gfx950-only
     auto* c = new ta_context();
     c->device = device;
+    c->cu_count = (uint32_t)std::max(1, prop.multiProcessorCount);
     if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking) != hipSuccess ||
@@ -138,7 +139,10 @@ int ta_context_create(int device, ta_context** out) {
         hipEventCreateWithFlags(&c->ev_tb_done, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fill, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_slot[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_slot[1], hipEventDisableTiming) != hipSuccess) {
         delete c;
         return TA_ERR_DEVICE;
     }
@@ -150,7 +154,7 @@ void ta_context_destroy(ta_context* ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     for (auto* b : {&ctx->qbytes, &ctx->tbytes, &ctx->qoff, &ctx->toff, &ctx->score, &ctx->tb, &ctx->slots,
-                    &ctx->cstart, &ctx->clen, &ctx->dst_off, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd})
+                    &ctx->cstart, &ctx->clen, &ctx->dst_off, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd, &ctx->ws_ptrs2})
         if (b->p) (void)hipFree(b->p);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     if (ctx->aux) (void)hipStreamDestroy(ctx->aux);
@@ -161,6 +165,8 @@ void ta_context_destroy(ta_context* ctx) {
     if (ctx->ev_join2) (void)hipEventDestroy(ctx->ev_join2);
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    for (hipEvent_t e : {ctx->ev_fill, ctx->ev_slot[0], ctx->ev_slot[1]})
+        if (e) (void)hipEventDestroy(e);
     delete ctx;
 }
 
@@ -385,8 +391,9 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     up(upload(ctx, &pl->d_bnd_off, bnd_off));
     up(upload(ctx, &pl->d_slot_off, pl->slot_off));
     if (rc == TA_OK && n_pairs) {
-        if (hipMalloc(&pl->d_goal_i, n_pairs * 4ull) != hipSuccess ||
-            hipMalloc(&pl->d_goal_j, n_pairs * 4ull) != hipSuccess)
+        // two halves: ta_plan_execute_batches alternates them between batches
+        if (hipMalloc(&pl->d_goal_i, 2 * n_pairs * 4ull) != hipSuccess ||
+            hipMalloc(&pl->d_goal_j, 2 * n_pairs * 4ull) != hipSuccess)
             rc = fail(ctx, TA_ERR_DEVICE, "hipMalloc goal");
     }
     if (rc == TA_OK && pl->n_dual_pairs &&
@@ -408,16 +415,28 @@ uint32_t ta_plan_chunks(const ta_plan* pl) { return pl ? (uint32_t)pl->chunks.si
 uint32_t ta_plan_dual_pairs(const ta_plan* pl) { return pl ? pl->n_dual_pairs : 0; }
 uint32_t ta_plan_flex_pairs(const ta_plan* pl) { return pl ? (uint32_t)pl->flexes.size() : 0; }
 
-static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill, bool trace) {
+// slot 1 = the second code buffer and goal half (ta_plan_execute_batches);
+// tb_waves > 0 caps the traceback grid.
+static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill, bool trace,
+                      int slot = 0, uint32_t tb_waves = 0) {
     const auto& ch = pl->chunks[c];
     ta_context* ctx = pl->ctx;
+    ta_context::Buf& ws = slot ? ctx->ws_ptrs2 : ctx->ws_ptrs;
     if (pl->ws_ptr_dwords)
-        if (int r = grow(ctx, ctx->ws_ptrs, pl->ws_ptr_dwords * 4ull)) return r;
+        if (int r = grow(ctx, ws, pl->ws_ptr_dwords * 4ull)) return r;
     if (pl->ws_bnd_words)
         if (int r = grow(ctx, ctx->ws_bnd, pl->ws_bnd_words * 4ull)) return r;
-    uint32_t* d_ptrs = static_cast<uint32_t*>(ctx->ws_ptrs.p);
+    uint32_t* d_ptrs = static_cast<uint32_t*>(ws.p);
+    uint32_t* goal_i = pl->d_goal_i + (slot ? pl->n_pairs : 0);
+    uint32_t* goal_j = pl->d_goal_j + (slot ? pl->n_pairs : 0);
     int32_t* d_bnd = static_cast<int32_t*>(ctx->ws_bnd.p);
     if (fill) {
+        // The flexible fill's pass hand-off records live in this buffer and are
+        // recognised by their tag alone, so whatever an earlier user of the
+        // memory left there (traceback codes of a freed workspace, other
+        // plans' records) must not survive: zero it (tag 0 is never valid)
+        // before any kernel of this chunk is enqueued.
+        if (ch.fcount && pl->ws_bnd_words) TA_HIP(ctx, hipMemsetAsync(d_bnd, 0, pl->ws_bnd_words * 4ull, s));
         ta::FillArgs a{};
         a.order = pl->d_order;
         a.begin = ch.begin;
@@ -437,8 +456,8 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         a.bnd_off = pl->d_bnd_off;
         a.score = io->score;
         a.target_begin = io->target_begin;
-        a.goal_i = pl->d_goal_i;
-        a.goal_j = pl->d_goal_j;
+        a.goal_i = goal_i;
+        a.goal_j = goal_j;
         a.fused = (pl->fused && pl->want_cigar) ? 1 : 0;
         a.slots = io->cigar_slots;
         a.slot_off = pl->d_slot_off;
@@ -517,13 +536,13 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         t.tlen = pl->d_tlen;
         t.ptrs = d_ptrs;
         t.ptr_off = pl->d_ptr_off;
-        t.goal_i = pl->d_goal_i;
-        t.goal_j = pl->d_goal_j;
+        t.goal_i = goal_i;
+        t.goal_j = goal_j;
         t.slots = io->cigar_slots;
         t.slot_off = pl->d_slot_off;
         t.cigar_start = io->cigar_start;
         t.cigar_len = io->cigar_len;
-        TA_HIP(pl->ctx, ta::launch_traceback(pl->type, t, s));
+        TA_HIP(pl->ctx, ta::launch_traceback(pl->type, t, s, tb_waves));
     }
     return TA_OK;
 }
@@ -564,6 +583,67 @@ int ta_plan_execute(ta_plan* pl, const ta_device_io* io, void* stream) {
     TA_HIP(ctx, hipEventRecord(ctx->ev_tb_done, ctx->tbs));
     TA_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_tb_done, 0));
     return TA_OK;
+}
+
+// Batches of one plan back to back with batch k's traceback (SALU-bound) on
+// the context's traceback stream beside batch k+1's fill (VALU-bound) on the
+// caller's stream.  Codes and goal cells alternate between two buffers; a fill
+// waits only for the traceback that last read its buffer.  TA_TB_WAVES_PER_SIMD
+// > 0 caps the traceback grid so it fits next to the fill's waves (dual fill:
+// 5 waves x 88 VGPRs per SIMD, traceback 32 VGPRs); the last unit runs
+// uncapped.  Default 0 (uncapped): on config 2 a capped traceback is
+// latency-bound and starved of VALU issue by the fill, and ends after it
+// (2 waves/SIMD: 3.88 ms per batch vs 3.44 unpipelined).
+int ta_plan_execute_batches(ta_plan* pl, const ta_device_io* ios, uint32_t n_batches, void* stream) {
+    if (!pl || (n_batches && !ios)) return TA_ERR_ARG;
+    for (uint32_t b = 0; b < n_batches; ++b)
+        if (int r = check_io(pl, ios + b)) return r;
+    ta_context* ctx = pl->ctx;
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    hipStream_t s = (hipStream_t)stream;  // NULL = the HIP null stream
+    const uint32_t nc = (uint32_t)pl->chunks.size();
+    const uint64_t units = (uint64_t)n_batches * nc;
+    bool pipe = pl->want_cigar && !pl->fused && !pl->staged && units >= 2 && pl->ws_ptr_dwords;
+    // both code buffers must fit; otherwise the batches run one after the other
+    if (pipe && grow(ctx, ctx->ws_ptrs2, pl->ws_ptr_dwords * 4ull) != TA_OK) {
+        pipe = false;
+        (void)hipGetLastError();  // the failed allocation is not an error here
+        ctx->last_error.clear();
+    }
+    if (!pipe) {
+        for (uint32_t b = 0; b < n_batches; ++b)
+            if (int r = ta_plan_execute(pl, ios + b, stream)) return r;
+        return TA_OK;
+    }
+    uint32_t per_simd = 0;
+    if (const char* e = std::getenv("TA_TB_WAVES_PER_SIMD")) per_simd = (uint32_t)std::max(0, std::atoi(e));
+    const uint32_t cap = per_simd * 4u * ctx->cu_count;  // 0 = uncapped
+    TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
+    TA_HIP(ctx, hipStreamWaitEvent(ctx->tbs, ctx->ev_fork, 0));  // tracebacks after earlier work on s
+    for (uint64_t u = 0; u < units; ++u) {
+        const int slot = (int)(u & 1);
+        const uint32_t b = (uint32_t)(u / nc), c = (uint32_t)(u % nc);
+        if (u >= 2) TA_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_slot[slot], 0));  // unit u-2's traceback is done
+        if (int r = exec_chunk(pl, ios + b, s, c, true, false, slot)) return r;
+        TA_HIP(ctx, hipEventRecord(ctx->ev_fill, s));
+        TA_HIP(ctx, hipStreamWaitEvent(ctx->tbs, ctx->ev_fill, 0));
+        if (int r = exec_chunk(pl, ios + b, ctx->tbs, c, false, true, slot, u + 1 < units ? cap : 0)) return r;
+        TA_HIP(ctx, hipEventRecord(ctx->ev_slot[slot], ctx->tbs));
+    }
+    TA_HIP(ctx, hipEventRecord(ctx->ev_tb_done, ctx->tbs));
+    TA_HIP(ctx, hipStreamWaitEvent(s, ctx->ev_tb_done, 0));
+    return TA_OK;
+}
+
+int ta_plan_check(ta_plan* pl) {
+    if (!pl) return TA_ERR_ARG;
+    if (!pl->d_err) return TA_OK;
+    uint32_t err = 0;
+    TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
+    TA_HIP(pl->ctx, hipMemcpy(&err, pl->d_err, 4, hipMemcpyDeviceToHost));
+    if (!err) return TA_OK;
+    TA_HIP(pl->ctx, hipMemset(pl->d_err, 0, 4));
+    return fail(pl->ctx, TA_ERR_DEVICE, "flexible fill: a pass hand-off poll timed out; results of this plan are invalid");
 }
 
 int ta_plan_execute_fill(ta_plan* pl, const ta_device_io* io, void* stream, uint32_t chunk) {
@@ -714,8 +794,9 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
     const int rc = host_batch(ctx, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, qend, tend, want_cigar, score,
                               target_begin, arena, arena_bytes, cigar_off, cigar_len, pl->slots_bytes,
                               [&](const ta_device_io* io, hipStream_t s) { return ta_plan_execute(pl, io, s); });
+    const int rc2 = rc == TA_OK ? ta_plan_check(pl) : rc;  // host_batch synchronised the stream
     ta_plan_destroy(pl);
-    return rc;
+    return rc2;
 }
 
 int ta_align_batch_affine(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff,

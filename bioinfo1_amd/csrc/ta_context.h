@@ -32,5 +32,10 @@ struct ta_context {
     // context and grown at execute time (a plan's chunks are sized by its
     // budget): plans of one context must not execute concurrently.
     Buf ws_ptrs, ws_bnd;
+    // Second traceback-code buffer for ta_plan_execute_batches: batch k+1's
+    // fill writes one while batch k's traceback reads the other.
+    Buf ws_ptrs2;
+    hipEvent_t ev_fill = nullptr, ev_slot[2] = {nullptr, nullptr};
+    uint32_t cu_count = 256;
     uint32_t epoch = 0;  // flexible-fill launches so far (tags of their pass hand-off records)
 };

@@ -374,7 +374,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
     const uint64_t rb = 2ull * (M + 1);
     io.rec_w = last_pass ? nullptr : rec + (pass & 1u) * rb;
     io.rec_r = pass ? rec + ((pass - 1u) & 1u) * rb : nullptr;
-    io.tag_w = a.epoch * 64u + pass + 1u;  // never 0, unique per launch and pass
+    // never 0, unique per launch and pass; the host zeroes the record buffers
+    // before each launch, so a record carries this tag only once written here
+    io.tag_w = a.epoch * 64u + pass + 1u;
     io.tag_r = a.epoch * 64u + pass;
     io.err = a.err;
     const FlexOut o = flex_pass_nv<MODE, CIGAR>(a, io, pass, last_pass, tdash, lane);

@@ -110,7 +110,8 @@ struct CompactArgs {
 hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_fill_mode(bool wide, const FillArgs& a, hipStream_t s);
-hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s);
+// max_waves > 0 caps the grid (the kernel strides over the pairs)
+hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, uint32_t max_waves = 0);
 // Dual-pair packed int16 fill (ta_dual.hip): a.order holds 2 pair ids per wave.
 hipError_t launch_dual(int mode, bool cigar, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>

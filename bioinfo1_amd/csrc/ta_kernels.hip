@@ -388,18 +388,23 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
 #ifdef TA_TU_MISC
 template <int MODE>
 __global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
+    // Wave-strided over the pairs: one wave per pair when the grid covers
+    // them all, fewer resident waves (each walking several pairs) when the
+    // launch is capped so it fits beside the next batch's fill (see
+    // ta_plan_execute_batches).
     const int lane = threadIdx.x & 63;
-    const uint32_t widx = wave_id();
-    if (widx >= a.count) return;
-    const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
-    const uint32_t n = a.qlen[p], m = a.tlen[p];
-    uint64_t st;
-    uint32_t len;
-    traceback_pair<MODE>(a.ptrs + a.ptr_off[p], n, m, a.goal_i[p], a.goal_j[p], a.slots + a.slot_off[p],
-                         cigar_slot_bytes(n, m), lane, &st, &len);
-    if (lane == 0) {
-        a.cigar_start[p] = a.slot_off[p] + st;
-        a.cigar_len[p] = len;
+    const uint32_t stride = gridDim.x * kWavesPerBlock;
+    for (uint32_t widx = wave_id(); widx < a.count; widx += stride) {
+        const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
+        const uint32_t n = a.qlen[p], m = a.tlen[p];
+        uint64_t st;
+        uint32_t len;
+        traceback_pair<MODE>(a.ptrs + a.ptr_off[p], n, m, a.goal_i[p], a.goal_j[p], a.slots + a.slot_off[p],
+                             cigar_slot_bytes(n, m), lane, &st, &len);
+        if (lane == 0) {
+            a.cigar_start[p] = a.slot_off[p] + st;
+            a.cigar_len[p] = len;
+        }
     }
 }
 
@@ -502,9 +507,9 @@ bool fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {
     return hi <= 32000 && lo >= -32000;
 }
 
-hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s) {
+hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, uint32_t max_waves) {
     if (!a.count) return hipSuccess;
-    const dim3 g = grid_for(a.count), b(kBlock);
+    const dim3 g = grid_for(max_waves ? std::min(a.count, max_waves) : a.count), b(kBlock);
     switch (mode) {
         case kGlobal: hipLaunchKernelGGL(traceback_kernel<kGlobal>, g, b, 0, s, a); break;
         case kLocal: hipLaunchKernelGGL(traceback_kernel<kLocal>, g, b, 0, s, a); break;

@@ -353,6 +353,9 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
             if (total) TM_HIP(ctx, hipMemcpyAsync(arena, ctx->m_cdst.p, total, hipMemcpyDeviceToHost, s));
         }
         TM_HIP(ctx, hipStreamSynchronize(s));
+        if (int r = ta_plan_check(plan))
+            return fail(ctx, TM_ERR_DEVICE, std::string("ta_plan_check: ") + ta_last_error(ctx->ta) + " (" +
+                                                ta_status_string(r) + ")");
         for (uint32_t p = 0; p < P; ++p) {
             const uint32_t r = pair_read[p];
             score[r] = sc[p];

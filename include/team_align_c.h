@@ -119,6 +119,22 @@ typedef struct ta_device_io {
  * null stream, as everywhere in HIP).  Asynchronous: returns after enqueueing. */
 int ta_plan_execute(ta_plan* plan, const ta_device_io* io, void* hip_stream);
 
+/* Enqueue n_batches executions of the plan, batch b with ios[b] (same
+ * lengths and scoring; e.g. a mapper's successive read chunks), pipelined:
+ * batch b's traceback runs on an internal stream beside batch b+1's fill,
+ * with the traceback codes double-buffered (when two code workspaces fit in
+ * HBM; else the batches run one after the other).  Every batch's results are
+ * complete when hip_stream reaches the end of the enqueued work.  Per batch
+ * the results are exactly ta_plan_execute's.  No reference counterpart: the
+ * reference aligns one pair per team::Align call (team_mapper.cpp:666-678). */
+int ta_plan_execute_batches(ta_plan* plan, const ta_device_io* ios, uint32_t n_batches, void* hip_stream);
+
+/* After the plan's executions have completed (stream synchronised): TA_OK, or
+ * TA_ERR_DEVICE when a kernel reported an internal failure since the last
+ * check (the flexible fill's bounded pass hand-off poll gave up; see
+ * ta_last_error).  Clears the flag.  ta_align_batch checks it itself. */
+int ta_plan_check(ta_plan* plan);
+
 /* Enqueue only the DP fill (scores/target_begin; traceback pointers into the
  * workspace) or only the traceback, for profiling the two kernels. */
 int ta_plan_execute_fill(ta_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);

@@ -326,3 +326,49 @@ def test_staged_plans(aligner, oracle, monkeypatch, mode):
         np.testing.assert_array_equal(r.scores, want.scores)
         assert r.cigars() == want.cigars()
         plan.close()
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2])
+def test_pipelined_batches(aligner, oracle, monkeypatch, mode):
+    """ta_plan_execute_batches (batch k's traceback beside batch k+1's fill,
+    double-buffered codes and goal cells, capped traceback grid): every
+    batch's outputs equal the oracle's, for one-chunk and chunked plans and
+    for the uncapped / capped traceback grid."""
+    b = synth.related_batch(300, 400, 380, seed=91 + mode)
+    want = oracle.align_batch(b, mode, 1, -1, -1, True)
+    for budget, per_simd in ((0, "2"), (0, "0"), (40 * 443 * 256, "1")):  # last: ~40 pairs per chunk
+        monkeypatch.setenv("TA_TB_WAVES_PER_SIMD", per_simd)
+        plan = DevicePlan(aligner, b, mode, 1, -1, -1, True, workspace_budget=budget)
+        assert (plan.chunks > 1) == (budget != 0)
+        outs = [plan.output_set() for _ in range(5)]
+        plan.run_batches(outs)
+        plan.run_batches(outs[:1])  # a single batch: the unpipelined path
+        for k, o in enumerate(outs):
+            r = o.results()
+            np.testing.assert_array_equal(r.scores, want.scores, err_msg=f"batch {k}")
+            np.testing.assert_array_equal(r.target_begins, want.target_begins)
+            assert r.cigars() == want.cigars(), (mode, budget, per_simd, k)
+        plan.close()
+
+
+def test_flex_records_ignore_stale_workspace():
+    """Regression: on a fresh context, this digest sequence once left traceback
+    codes in freed memory that the next ws_bnd allocation reused, and two
+    stale dwords carried the flexible fill's small hand-off tags (epoch 3):
+    ragged_global's first run read them as pass-0 records (2/2000 scores
+    wrong).  The host now zeroes the record buffers before each flex launch."""
+    al = Aligner(0)
+    try:
+        for name in ("cfg2_local", "cfg2_related_local", "g1k_global", "s1k_semi", "ragged_local", "ragged_semi"):
+            meta, _ = load_digest(name)
+            for cig in (True, False):
+                al.align_batch(digest_batch(name), meta["type"], meta["match"], meta["mismatch"], meta["gap"], cig)
+        meta, d = load_digest("ragged_global")
+        batch = digest_batch("ragged_global")
+        for cig in (True, False):
+            r = al.align_batch(batch, meta["type"], meta["match"], meta["mismatch"], meta["gap"], cig)
+            np.testing.assert_array_equal(r.scores, d["scores"])
+            if cig:
+                np.testing.assert_array_equal(r.cigar_lens, d["cigar_lens"])
+    finally:
+        al.close()
