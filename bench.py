@@ -464,7 +464,8 @@ def main():
         traffic = load_traffic(tag)
         roof = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
                 "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": traffic, "kernel": "affine_fill_kernel" if args.gap_open is not None else "fill_kernel",
+                "traffic": traffic, "kernel": ("affine_dual_fill_kernel" if plan.dual_pairs else "affine_fill_kernel")
+                if args.gap_open is not None else "fill_kernel",
                 "kernel_ms": round(fill_ms, 4),
                 "alg_bytes_per_launch": alg,
                 "note": "integer DP: VALU-bound, not HBM- or MFMA-bound (see valu)"}

@@ -102,6 +102,8 @@ def lib() -> C.CDLL:
         getattr(L, f).argtypes = [C.c_void_p]
     L.ta_affine_plan_chunks.restype = C.c_uint32
     L.ta_affine_plan_chunks.argtypes = [C.c_void_p]
+    L.ta_affine_plan_dual_pairs.restype = C.c_uint32
+    L.ta_affine_plan_dual_pairs.argtypes = [C.c_void_p]
     L.ta_affine_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ta_affine_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     L.ta_affine_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
@@ -115,7 +117,7 @@ ABI_SYMBOLS = [
     "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes",
     "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_execute", "ta_plan_execute_batches", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_execute_traceback",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
-    "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
+    "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
     "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
 ]
 # The drop-in C++ entry point (team_alignment.hpp), g++/libstdc++ cxx11 mangling.
@@ -341,7 +343,7 @@ class DevicePlan:
                             self.slots.data_ptr(), self.cigar_start.data_ptr(), self.cigar_len.data_ptr())
         self.workspace_bytes = int(self._fn("ta_plan_workspace_bytes")(h))
         self.chunks = int(self._fn("ta_plan_chunks")(h))
-        self.dual_pairs = 0 if self.affine else int(L.ta_plan_dual_pairs(h))
+        self.dual_pairs = int(L.ta_affine_plan_dual_pairs(h)) if self.affine else int(L.ta_plan_dual_pairs(h))
         self.flex_pairs = 0 if self.affine else int(L.ta_plan_flex_pairs(h))
 
     def _stream(self):

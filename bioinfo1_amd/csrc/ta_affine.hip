@@ -40,6 +40,7 @@
 #include "../../include/team_align_c.h"
 #include "ta_context.h"
 #include "ta_device.h"
+#include "ta_packed.h"
 
 namespace ta {
 namespace {
@@ -68,6 +69,9 @@ struct AffArgs {
     const uint64_t* slot_off;
     uint64_t* cigar_start;
     uint32_t* cigar_len;
+    const uint32_t* count_dev;  // non-null: wave count read on the device (the dual fill's hand-back list)
+    uint32_t* fb_list;          // dual fill: couples handed back to the int32 fill ('-' in a query)
+    uint32_t* fb_count;
 };
 
 // 64 boundary entries per chunk: column 64k+lane+1.
@@ -296,7 +300,7 @@ template <int MODE, bool CIGAR>
 __global__ __launch_bounds__(kBlock) void affine_fill_kernel(AffArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t widx = wave_id();
-    if (widx >= a.count) return;  // wave-uniform
+    if (widx >= (a.count_dev ? *a.count_dev : a.count)) return;  // wave-uniform
     const uint32_t p = a.order[a.begin + widx];
     const uint32_t n = a.qlen[p], m = a.tlen[p];
     const int O = a.open, X = a.extend;
@@ -457,7 +461,341 @@ __global__ __launch_bounds__(kBlock) void affine_traceback_kernel(AffArgs a) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Packed two-pair affine fill (global / semi-global): two pairs of the same
+// (n, m) per wave, pair A in bits 15:0 and pair B in bits 31:16 of every
+// register, v_pk_* arithmetic.  Same geometry and the same 4-bit codes as
+// affine_fill_kernel, so the traceback is shared.  Values are stored biased
+// by -ma*j (H, E and F alike: S = V - ma*j), which turns the diagonal
+// candidate into one v_pk_mad_i16 of the mismatch flag (ta_dual.hip) and the
+// horizontal ones into adds of (go - ma, ge - ma); vertical steps keep the
+// bias.  The -inf of E(i,0) / F(0,j) is replaced by H - K with K > |open| +
+// |ext|: it loses every comparison there, as -inf does, and stays in range.
+// Codes: every compare is the sign of a saturating packed difference, spread
+// to bytes by v_perm and inserted by v_bfi (ta_packed.h): x = [D | I] planes
+// from (f > m1, e > diag), y = [F-ext | E-ext] planes from (fe > fo, ee > eo).
+// The host sends only couples whose every value provably fits int16
+// (affine_fits_int16); a couple with '-' in a query goes back to the int32
+// fill through fb_list.
+template <int MODE, bool CIGAR, int NV>
+__device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* const (&Q)[2], const uint8_t* const (&T)[2],
+                                              uint2* const (&ptrs)[2], uint2* B, uint32_t n, uint32_t m, uint32_t pass,
+                                              bool last_pass, bool tdash, int lane, PassOut (&out)[2]) {
+    constexpr int R = kRows;
+    const int ma = a.match, mi = a.mismatch, O = a.open, X = a.extend;
+    const int OX = O + X;
+    const int K = abs(O) + abs(X) + 2;  // E(i,0) = H(i,0) - K, F(0,j) = H(0,j) - K
+    const uint32_t KD = rep16(mi - ma);
+    const uint32_t GOQ = rep16(OX), GEQ = rep16(X);  // vertical (no '-' in these queries)
+    uint32_t ONE = 0x00010001u;
+    asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16 (ta_packed.h)
+    const uint32_t Tmax = pass_steps(m);
+    const uint32_t row_base = pass * kPassRows;
+    const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
+    const uint32_t nl = (nrows + R - 1) / R;
+    const bool has_next = !last_pass;
+    const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
+
+    uint32_t q2[R], H2[R], E2[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i0 = row_base + (uint32_t)lane * R + r;  // row i0 + 1
+        q2[r] = i0 < n ? ((uint32_t)Q[0][i0] | ((uint32_t)Q[1][i0] << 16)) : 0u;
+        const int h0 = (MODE == kGlobal) ? O + (int)(i0 + 1) * X : 0;  // H(i, 0)
+        H2[r] = rep16(h0);
+        E2[r] = rep16(h0 - K);
+    }
+    const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
+    uint32_t recvH = rep16((MODE == kGlobal && ia) ? O + (int)ia * X : 0);  // H(ia, 0)
+    uint32_t recvF = 0, Flast = 0;
+    uint32_t tc2 = 0;
+    uint32_t maj = rep16(-ma * lane);  // ma*j at t = -1 (semi: row n holds H = S + ma*j)
+    const uint32_t MA2 = rep16(ma);
+    uint32_t jj = rep16(-lane);
+    uint32_t rowbest = rep16(-32768), rowbest_j = 0;
+
+    uint32_t tcur[2], tnext[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        tcur[h] = load_tchunk(T[h], m, 0, lane);
+        tnext[h] = load_tchunk(T[h], m, 1, lane);
+    }
+    uint2 bcur = make_uint2(0, 0), bnext = make_uint2(0, 0);
+    auto load_b = [&](uint32_t k) {
+        const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+        return j <= m ? B[j] : make_uint2(0, 0);
+    };
+    if (pass > 0) {
+        bcur = load_b(0);
+        bnext = load_b(1);
+    }
+    const uint32_t steps = m + nl - 1;
+    uint2* prow0 = CIGAR ? ptrs[0] + (uint64_t)pass * Tmax * kWave : nullptr;
+    uint2* prow1 = CIGAR ? ptrs[1] + (uint64_t)pass * Tmax * kWave : nullptr;
+
+    auto reload = [&](uint32_t t) {
+        if ((t & 255u) == 0) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                tcur[h] = tnext[h];
+                tnext[h] = load_tchunk(T[h], m, (t >> 8) + 1, lane);
+            }
+        }
+        if (pass > 0) {
+            bcur = bnext;
+            bnext = load_b((t >> 6) + 1);
+        }
+    };
+    auto step = [&](uint32_t t, auto masked_tag) {
+        constexpr bool MASKED = decltype(masked_tag)::value;
+        uint32_t topH, topF;
+        if (pass == 0) {  // row 0 (:89-92 with an affine gap): H(0,j) - ma*j; F(0,j) = -inf stand-in
+            const int jt = (int)t + 1;
+            const int h0 = ((MODE == kGlobal) ? O + jt * X : 0) - ma * jt;
+            topH = rep16(h0);
+            topF = rep16(h0 - K);
+        } else {
+            topH = (uint32_t)rdlane((int)bcur.x, t & 63u);
+            topF = (uint32_t)rdlane((int)bcur.y, t & 63u);
+        }
+        const uint32_t sh = (t & 3u) * 8;
+        const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
+        const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
+        const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
+        const uint32_t prev = recvH;
+        recvH = (uint32_t)wave_shr1((int)topH, (int)H2[R - 1]);
+        recvF = (uint32_t)wave_shr1((int)topF, (int)Flast);
+        tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        jj = pk_add(jj, ONE);
+        if (MODE == kSemi) maj = pk_add(maj, MA2);
+
+        const int j = (int)t - lane + 1;
+        const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
+        uint32_t ax0 = 0, ax1 = 0, ay0 = 0, ay1 = 0;
+        if (active) {
+            uint32_t GOT = rep16(OX - ma), GET = rep16(X - ma);  // horizontal, biased
+            if (tdash) {
+                const bool da = (tc2 & 0xFFFFu) == '-', db = (tc2 >> 16) == '-';
+                GOT = ((uint32_t)(da ? -ma : OX - ma) & 0xFFFFu) | ((uint32_t)(db ? -ma : OX - ma) << 16);
+                GET = ((uint32_t)(da ? -ma : X - ma) & 0xFFFFu) | ((uint32_t)(db ? -ma : X - ma) << 16);
+            }
+            auto e_of = [&](int r) { return pk_min_u16(q2[r] ^ tc2, ONE); };
+            uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
+            uint32_t upH = recvH, upF = recvF;
+            static_for<0, R>([&](auto rc) {
+                constexpr int r = decltype(rc)::value;
+                const uint32_t old = H2[r];
+                const uint32_t diag = dnext;
+                if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
+                const uint32_t eo = pk_add(old, GOT), ee = pk_add(E2[r], GET);
+                const uint32_t e = pk_max(eo, ee);
+                const uint32_t fo = pk_add(upH, GOQ), fe = pk_add(upF, GEQ);
+                const uint32_t f = pk_max(fo, fe);
+                const uint32_t m1 = pk_max(diag, e);
+                const uint32_t h = pk_max(m1, f);
+                if (CIGAR) {
+                    const uint32_t wi = pk_sub_sat(diag, e);  // sign: e > diag   (INSERT)
+                    const uint32_t wd = pk_sub_sat(m1, f);    // sign: f > m1     (DELETE)
+                    const uint32_t xe = pk_sub_sat(eo, ee);   // sign: ee > eo    (E extends)
+                    const uint32_t xf = pk_sub_sat(fo, fe);   // sign: fe > fo    (F extends)
+                    uint32_t& ax = (r < 8) ? ax0 : ax1;
+                    uint32_t& ay = (r < 8) ? ay0 : ay1;
+                    ax = bfi(0x01010101u << (7 - (r & 7)), sign_bytes(wd, wi), ax);
+                    ay = bfi(0x01010101u << (7 - (r & 7)), sign_bytes(xf, xe), ay);
+                }
+                E2[r] = e;
+                H2[r] = h;
+                upH = h;
+                upF = f;
+            });
+            Flast = upF;
+            if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + ma*j, strict '>' (:271-278)
+                const uint32_t v = pk_add(H2[NV - 1], maj);
+                rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jj, rowbest_j);
+                rowbest = pk_max(rowbest, v);
+            }
+            if (has_next && (uint32_t)lane == nl - 1) B[j] = make_uint2(H2[R - 1], Flast);
+        }
+        if (CIGAR) {
+            const uint32_t off = t * kWave + (uint32_t)lane;
+            prow0[off] = make_uint2(__builtin_amdgcn_perm(ax0, ax1, 0x06020400u), __builtin_amdgcn_perm(ay0, ay1, 0x06020400u));
+            prow1[off] = make_uint2(__builtin_amdgcn_perm(ax0, ax1, 0x07030501u), __builtin_amdgcn_perm(ay0, ay1, 0x07030501u));
+        }
+    };
+    const uint32_t ramp_end = min(nl - 1, steps);
+    const uint32_t every = (pass > 0) ? 64u : 256u;
+    uint32_t t = 0, next_reload = every;
+    auto run_steps = [&](uint32_t t_end, auto masked_tag) {
+        while (t < t_end) {
+            if (t == next_reload) {
+                reload(t);
+                next_reload += every;
+            }
+            const uint32_t blk = min(t_end, next_reload);
+            for (; t < blk; ++t) step(t, masked_tag);
+        }
+    };
+    run_steps(ramp_end, std::true_type{});
+    run_steps(m, std::false_type{});
+    run_steps(steps, std::true_type{});
+
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        PassOut& o = out[h];
+        o = PassOut{INT_MIN, 0, 0, INT_MIN, 0, 0};
+        if (MODE == kSemi) {
+            // column m: H = S + ma*m for every row, so S orders them; first lane, then first row (:265-270)
+            int cv = INT_MIN;
+            uint32_t cr = 0;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const int sv = h ? hi16(H2[r]) : lo16(H2[r]);
+                if ((uint32_t)r < nv_lane && sv > cv) {
+                    cv = sv;
+                    cr = r;
+                }
+            }
+            const int mx = wave_max(cv);
+            const int fl = first_lane(cv == mx && nv_lane > 0);
+            o.h = mx + ma * (int)m;
+            o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane((int)cr, fl) + 1;
+            o.j = m;
+            if (last_pass) {
+                o.row_h = rdlane(h ? hi16(rowbest) : lo16(rowbest), nl - 1);  // -32768: never set
+                o.row_j = (uint32_t)rdlane((int)(h ? (rowbest_j >> 16) : (rowbest_j & 0xFFFFu)), nl - 1);
+            }
+        } else if (last_pass) {
+            int hv[R];
+#pragma unroll
+            for (int r = 0; r < R; ++r) hv[r] = h ? hi16(H2[r]) : lo16(H2[r]);
+            o.corner = rdlane(select_row<R>(hv, nrows - (nl - 1) * R - 1), nl - 1) + ma * (int)m;
+        }
+    }
+}
+
+template <int MODE, bool CIGAR>
+__device__ __forceinline__ void aff_dual_pass_nv(const AffArgs& a, const uint8_t* const (&Q)[2],
+                                                 const uint8_t* const (&T)[2], uint2* const (&ptrs)[2], uint2* B,
+                                                 uint32_t n, uint32_t m, uint32_t pass, bool last_pass, bool tdash,
+                                                 int lane, PassOut (&out)[2]) {
+    const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
+    const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
+    if (MODE == kGlobal || nv == kRows || !last_pass)
+        return aff_dual_pass<MODE, CIGAR, kRows>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
+#define TA_NV_CASE(k) \
+    case k: return aff_dual_pass<MODE, CIGAR, k>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
+    switch (nv) {
+        TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
+        TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
+        default: TA_NV_CASE(15)
+    }
+#undef TA_NV_CASE
+}
+
+// order: 2 pair ids per wave (same n and m, values within int16)
+template <int MODE, bool CIGAR>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void affine_dual_fill_kernel(AffArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t widx = wave_id();
+    if (widx >= a.count) return;
+    uint32_t p[2];
+    p[0] = a.order[2 * (a.begin + widx)];
+    p[1] = a.order[2 * (a.begin + widx) + 1];
+    const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
+    const uint8_t* Q[2];
+    const uint8_t* T[2];
+    uint2* ptrs[2];
+    bool tdash = false, qdash = false;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        Q[h] = a.qbytes + a.qoff[p[h]];
+        T[h] = a.tbytes + a.toff[p[h]];
+        ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
+        for (uint32_t k = (uint32_t)lane; k < m; k += 64) tdash |= T[h][k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < n; k += 64) qdash |= Q[h][k] == '-';
+    }
+    if (__ballot(qdash)) {  // per-row vertical gap constants: the int32 fill takes the couple
+        if (lane == 0) {
+            const uint32_t at = atomicAdd(a.fb_count, 2u);
+            a.fb_list[at] = p[0];
+            a.fb_list[at + 1] = p[1];
+        }
+        return;
+    }
+    tdash = __ballot(tdash) != 0;
+    const uint32_t passes = n_passes(n);
+    uint2* B = (passes > 1) ? reinterpret_cast<uint2*>(a.bnd + a.bnd_off[p[0]]) : nullptr;
+    int best_h[2], corner[2] = {0, 0};
+    uint32_t best_i[2], best_j[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        best_h[h] = (MODE == kSemi) ? 0 : INT_MIN;  // semi starts from (0,m), cost 0
+        best_i[h] = 0;
+        best_j[h] = (MODE == kSemi) ? m : 0;
+    }
+    for (uint32_t pass = 0; pass < passes; ++pass) {
+        const bool last_pass = pass + 1 == passes;
+        PassOut o[2];
+        aff_dual_pass_nv<MODE, CIGAR>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, o);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (MODE == kSemi && o[h].h > best_h[h]) {  // strict: the upper pass wins ties
+                best_h[h] = o[h].h;
+                best_i[h] = o[h].i;
+                best_j[h] = o[h].j;
+            }
+            if (MODE == kSemi && last_pass && o[h].row_h > best_h[h]) {  // row n after column m (:271-278)
+                best_h[h] = o[h].row_h;
+                best_i[h] = n;
+                best_j[h] = o[h].row_j;
+            }
+            if (MODE == kGlobal && last_pass) corner[h] = o[h].corner;
+        }
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // boundary row -> next pass
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            a.score[p[h]] = (MODE == kGlobal) ? corner[h] : best_h[h];
+            a.target_begin[p[h]] = 0;
+            a.goal_i[p[h]] = (MODE == kGlobal) ? n : best_i[h];
+            a.goal_j[p[h]] = (MODE == kGlobal) ? m : best_j[h];
+        }
+    }
+}
+
 inline dim3 aff_grid(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock); }
+
+hipError_t launch_affine_dual(int mode, bool cigar, const AffArgs& a, hipStream_t s) {
+    if (a.count == 0) return hipSuccess;
+    const dim3 g = aff_grid(a.count), b(kBlock);
+    switch (mode * 2 + (cigar ? 1 : 0)) {
+        case kGlobal * 2: hipLaunchKernelGGL((affine_dual_fill_kernel<kGlobal, false>), g, b, 0, s, a); break;
+        case kGlobal * 2 + 1: hipLaunchKernelGGL((affine_dual_fill_kernel<kGlobal, true>), g, b, 0, s, a); break;
+        case kSemi * 2: hipLaunchKernelGGL((affine_dual_fill_kernel<kSemi, false>), g, b, 0, s, a); break;
+        case kSemi * 2 + 1: hipLaunchKernelGGL((affine_dual_fill_kernel<kSemi, true>), g, b, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// Every packed value of aff_dual_pass within int16, with margins: H from the
+// diagonal path below / any path above, E and F within one gap step of H, the
+// bias -ma*j, the -inf stand-ins (H - K) and one more step of candidates.
+bool affine_fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int open, int ext) {
+    if (mode == kLocal || n == 0 || m == 0) return false;
+    const long long N = n, M = m, mn = std::min(N, M), mx = std::max(N, M);
+    const long long lo_s = std::min({0LL, (long long)ma, (long long)mi});
+    const long long hi_s = std::max({0LL, (long long)ma, (long long)mi});
+    long long hlo = mn * lo_s;
+    if (mode == kGlobal) hlo += std::min(0LL, (long long)open) + mx * std::min(0LL, (long long)ext);
+    const long long hhi = mn * hi_s + (N + M) * (std::max(0LL, (long long)open) + std::max(0LL, (long long)ext));
+    const long long k = std::llabs(open) + std::llabs(ext) + 2;
+    const long long marg = 2 * k + 2 * std::llabs(ma) + std::llabs(mi) + 8;
+    const long long slo = hlo - std::max(0LL, (long long)ma) * M - marg;
+    const long long shi = hhi + std::max(0LL, -(long long)ma) * M + marg;
+    return slo >= -32000 && shi <= 32000;
+}
 
 hipError_t launch_affine_fill(int mode, bool cigar, const AffArgs& a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
@@ -500,14 +838,19 @@ struct ta_affine_plan {
     int type = 0, match = 0, mismatch = 0, open = 0, extend = 0;
     bool want_cigar = false;
     std::vector<uint32_t> order;  // pairs by descending cells: the big ones start first
+    std::vector<uint32_t> singles, duals;  // int32 fill: pairs; packed fill: 2 pair ids per couple
     std::vector<uint64_t> ptr_off, bnd_off, slot_off;
     struct Chunk {
-        uint32_t begin, count;  // plan order
+        uint32_t begin, count;    // plan order (traceback)
+        uint32_t sbegin, scount;  // singles
+        uint32_t dbegin, dcount;  // couples
         uint64_t ptr_entries, bnd_entries;
     };
     std::vector<Chunk> chunks;
     uint64_t slots_bytes = 0, ws_ptr_entries = 0, ws_bnd_entries = 0;
     uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr, *d_goal_i = nullptr, *d_goal_j = nullptr;
+    uint32_t *d_singles = nullptr, *d_duals = nullptr;
+    uint32_t* d_fb = nullptr;  // hand-back list [2 * couples], then one counter per chunk
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
 };
 
@@ -560,7 +903,8 @@ void ta_affine_plan_destroy(ta_affine_plan* pl) {
     if (!pl) return;
     (void)hipSetDevice(pl->ctx->device);
     for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_goal_i,
-                    (void*)pl->d_goal_j, (void*)pl->d_ptr_off, (void*)pl->d_bnd_off, (void*)pl->d_slot_off})
+                    (void*)pl->d_goal_j, (void*)pl->d_ptr_off, (void*)pl->d_bnd_off, (void*)pl->d_slot_off,
+                    (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_fb})
         if (p) (void)hipFree(p);
     delete pl;
 }
@@ -592,11 +936,29 @@ int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qle
     pl->open = gap_open;
     pl->extend = gap_extend;
     pl->want_cigar = want_cigar != 0;
-    pl->order.resize(n_pairs);
-    std::iota(pl->order.begin(), pl->order.end(), 0u);
-    std::stable_sort(pl->order.begin(), pl->order.end(), [&](uint32_t x, uint32_t y) {
-        return (uint64_t)qlen[x] * tlen[x] > (uint64_t)qlen[y] * tlen[y];
+    std::vector<uint32_t> byc(n_pairs);
+    std::iota(byc.begin(), byc.end(), 0u);
+    std::stable_sort(byc.begin(), byc.end(), [&](uint32_t x, uint32_t y) {
+        const uint64_t cx = (uint64_t)qlen[x] * tlen[x], cy = (uint64_t)qlen[y] * tlen[y];
+        if (cx != cy) return cx > cy;
+        return qlen[x] != qlen[y] ? qlen[x] > qlen[y] : tlen[x] > tlen[y];  // equal shapes adjacent
     });
+    // units: couples of equal shape for the packed fill (global / semi, values
+    // within int16; TA_AFFINE_DUAL=0 disables), else single pairs
+    bool dual_ok = true;
+    if (const char* e = std::getenv("TA_AFFINE_DUAL")) dual_ok = std::atoi(e) != 0;
+    std::vector<std::pair<uint32_t, uint32_t>> units;  // (a, b); b == UINT32_MAX: single
+    for (uint32_t k = 0; k < n_pairs;) {
+        const uint32_t x = byc[k];
+        if (dual_ok && k + 1 < n_pairs && qlen[byc[k + 1]] == qlen[x] && tlen[byc[k + 1]] == tlen[x] &&
+            ta::affine_fits_int16(type, qlen[x], tlen[x], match, mismatch, gap_open, gap_extend)) {
+            units.push_back({x, byc[k + 1]});
+            k += 2;
+        } else {
+            units.push_back({x, UINT32_MAX});
+            ++k;
+        }
+    }
     pl->slot_off.assign(n_pairs, 0);
     uint64_t so = 0;
     for (uint32_t p = 0; p < n_pairs; ++p) {
@@ -608,20 +970,33 @@ int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qle
     const uint64_t budget_entries = std::max<uint64_t>(budget / sizeof(uint2), 1);
     pl->ptr_off.assign(n_pairs, 0);
     pl->bnd_off.assign(n_pairs, 0);
-    ta_affine_plan::Chunk c{0, 0, 0, 0};
-    for (uint32_t k = 0; k < n_pairs; ++k) {
-        const uint32_t p = pl->order[k];
-        const uint64_t pe = pl->want_cigar ? ta::ptr_dwords(qlen[p], tlen[p]) : 0;
-        const uint64_t be = ta::bnd_words(qlen[p], tlen[p]);
+    ta_affine_plan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0};
+    for (const auto& u : units) {
+        const uint32_t ids[2] = {u.first, u.second};
+        const int cnt = u.second == UINT32_MAX ? 1 : 2;
+        uint64_t pe = 0;
+        for (int h = 0; h < cnt; ++h) pe += pl->want_cigar ? ta::ptr_dwords(qlen[ids[h]], tlen[ids[h]]) : 0;
         if (c.count && c.ptr_entries + pe > budget_entries) {
             pl->chunks.push_back(c);
-            c = {k, 0, 0, 0};
+            c = {(uint32_t)pl->order.size(), 0, (uint32_t)pl->singles.size(), 0, (uint32_t)(pl->duals.size() / 2), 0, 0, 0};
         }
-        pl->ptr_off[p] = c.ptr_entries;
-        pl->bnd_off[p] = c.bnd_entries;
-        c.ptr_entries += pe;
-        c.bnd_entries += be;
-        ++c.count;
+        for (int h = 0; h < cnt; ++h) {
+            const uint32_t p = ids[h];
+            pl->ptr_off[p] = c.ptr_entries;
+            pl->bnd_off[p] = c.bnd_entries;
+            c.ptr_entries += pl->want_cigar ? ta::ptr_dwords(qlen[p], tlen[p]) : 0;
+            c.bnd_entries += ta::bnd_words(qlen[p], tlen[p]);
+            pl->order.push_back(p);
+            ++c.count;
+        }
+        if (cnt == 2) {
+            pl->duals.push_back(u.first);
+            pl->duals.push_back(u.second);
+            ++c.dcount;
+        } else {
+            pl->singles.push_back(u.first);
+            ++c.scount;
+        }
     }
     if (c.count) pl->chunks.push_back(c);
     for (const auto& ch : pl->chunks) {
@@ -636,6 +1011,9 @@ int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qle
     up(aupload(ctx, &pl->d_qlen, ql));
     up(aupload(ctx, &pl->d_tlen, tl));
     up(aupload(ctx, &pl->d_order, pl->order));
+    up(aupload(ctx, &pl->d_singles, pl->singles));
+    up(aupload(ctx, &pl->d_duals, pl->duals));
+    if (!pl->duals.empty()) up(aupload(ctx, &pl->d_fb, std::vector<uint32_t>(pl->duals.size() + pl->chunks.size(), 0u)));
     up(aupload(ctx, &pl->d_ptr_off, pl->ptr_off));
     up(aupload(ctx, &pl->d_bnd_off, pl->bnd_off));
     up(aupload(ctx, &pl->d_slot_off, pl->slot_off));
@@ -657,6 +1035,7 @@ uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* pl) {
     return pl ? pl->ws_ptr_entries * sizeof(uint2) + pl->ws_bnd_entries * sizeof(int2) : 0;
 }
 uint32_t ta_affine_plan_chunks(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->chunks.size() : 0; }
+uint32_t ta_affine_plan_dual_pairs(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->duals.size() : 0; }
 
 static int affine_check_io(ta_affine_plan* pl, const ta_device_io* io) {
     if (!pl || !io) return TA_ERR_ARG;
@@ -700,7 +1079,31 @@ static int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStre
     a.slot_off = pl->d_slot_off;
     a.cigar_start = io->cigar_start;
     a.cigar_len = io->cigar_len;
-    if (fill) TA_AHIP(ctx, ta::launch_affine_fill(pl->type, pl->want_cigar, a, s));
+    if (fill) {
+        if (ch.dcount) {  // packed couples, then the couples they hand back, on the same stream
+            uint32_t* fb_list = pl->d_fb + 2ull * ch.dbegin;
+            uint32_t* fb_count = pl->d_fb + pl->duals.size() + c;
+            TA_AHIP(ctx, hipMemsetAsync(fb_count, 0, 4, s));
+            ta::AffArgs d = a;
+            d.order = pl->d_duals;
+            d.begin = ch.dbegin;
+            d.count = ch.dcount;
+            d.fb_list = fb_list;
+            d.fb_count = fb_count;
+            TA_AHIP(ctx, ta::launch_affine_dual(pl->type, pl->want_cigar, d, s));
+            ta::AffArgs f = a;
+            f.order = fb_list;
+            f.begin = 0;
+            f.count = 2 * ch.dcount;
+            f.count_dev = fb_count;
+            TA_AHIP(ctx, ta::launch_affine_fill(pl->type, pl->want_cigar, f, s));
+        }
+        ta::AffArgs sa = a;
+        sa.order = pl->d_singles;
+        sa.begin = ch.sbegin;
+        sa.count = ch.scount;
+        TA_AHIP(ctx, ta::launch_affine_fill(pl->type, pl->want_cigar, sa, s));
+    }
     if (trace && pl->want_cigar) TA_AHIP(ctx, ta::launch_affine_traceback(pl->type, a, s));
     return TA_OK;
 }

@@ -167,6 +167,9 @@ void ta_affine_plan_destroy(ta_affine_plan* plan);
 uint64_t ta_affine_plan_cigar_slots_bytes(const ta_affine_plan* plan);
 uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* plan);
 uint32_t ta_affine_plan_chunks(const ta_affine_plan* plan);
+/* Pairs the plan runs in the packed two-pairs-per-wave int16 affine fill
+ * (global / semi-global couples of equal shape whose values provably fit). */
+uint32_t ta_affine_plan_dual_pairs(const ta_affine_plan* plan);
 /* Enqueue the whole batch / one chunk's fill / one chunk's traceback on hip_stream. */
 int ta_affine_plan_execute(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream);
 int ta_affine_plan_execute_fill(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);

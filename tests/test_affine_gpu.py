@@ -135,3 +135,47 @@ def test_config5_size_property(aligner, oracle):
     sub = synth.related_batch(4, 10000, 10000, seed=0x5EED)
     want = oracle.align_affine_batch(sub, 2, *sc, True)
     _same(got, want, 4, "cfg5")
+
+
+def _shaped(P, shapes, alphabet, seed):
+    rng = np.random.default_rng(seed)
+    qa, ta = (alphabet, alphabet) if isinstance(alphabet, bytes) else alphabet
+    qa, ta = np.frombuffer(qa, np.uint8), np.frombuffer(ta, np.uint8)
+    pairs = []
+    for k in range(P):
+        n, m = shapes[k % len(shapes)]
+        pairs.append((qa[rng.integers(len(qa), size=n)].tobytes(), ta[rng.integers(len(ta), size=m)].tobytes()))
+    return synth.from_pairs(pairs)
+
+
+# (mode, (match, mismatch, open, extend), alphabet, shapes, pairs): equal-shape
+# couples for the packed int16 fill (global / semi); '-' in a target is handled
+# in the kernel, '-' in a query hands the couple back to the int32 fill
+DUAL_AFFINE = [
+    (2, (1, -1, -2, -1), b"ACGT", [(300, 280), (17, 900), (1000, 1000)], 60),
+    (0, (1, -1, -2, -1), b"ACGT", [(300, 280), (33, 64), (1024, 1000)], 60),
+    (2, (2, -3, -5, -2), b"ACGT-", [(500, 520), (1100, 900)], 24),
+    (2, (2, -3, -5, -2), (b"ACGT", b"ACGT-"), [(500, 520), (1100, 900)], 24),
+    (0, (1, -1, -3, -1), (b"ACGT", b"AC-"), [(1500, 1300), (64, 70)], 16),
+    (0, (2, -3, -5, -2), b"acgtN-", [(700, 650), (2100, 2000)], 12),
+    (2, (3, -1, -1, -1), b"ACGT", [(2049, 1900), (1031, 1500)], 12),
+    (0, (1, -1, 0, -1), b"ACGT", [(900, 950), (1500, 1400)], 16),
+    (2, (1, -2, 1, -3), b"AC", [(400, 380), (1030, 1030)], 20),
+]
+
+
+@pytest.mark.parametrize("case", range(len(DUAL_AFFINE)))
+def test_affine_dual_fill(aligner, oracle, case, monkeypatch):
+    mode, sc, alpha, shapes, P = DUAL_AFFINE[case]
+    b = _shaped(P, shapes, alpha, 0xAD0 + case)
+    plan = DevicePlan(aligner, b, mode, sc[0], sc[1], sc[3], True, gap_open=sc[2])
+    assert plan.dual_pairs == P, plan.dual_pairs
+    plan.close()
+    want = oracle.align_affine_batch(b, mode, *sc, True)
+    assert not want.status.any()
+    for dual in ("1", "0"):
+        monkeypatch.setenv("TA_AFFINE_DUAL", dual)
+        got = aligner.align_batch_affine(b, mode, *sc, True)
+        _same(got, want, P, (case, dual))
+        got0 = aligner.align_batch_affine(b, mode, *sc, False)
+        np.testing.assert_array_equal(got0.scores, want.scores)
