@@ -422,9 +422,14 @@ __device__ __forceinline__ void aff_traceback_pair(const uint2* P, uint32_t n, u
             } else if (iflag) {
                 state = 1;
             } else {
-                w.push('M', 1);
-                --i;
-                --j;
+                // a whole M run at once: lane L holds step tt0 + L of this stripe, i.e. the
+                // diagonal cell d = kk - L back (row r - d); the streak of M codes going down
+                // from lane kk is the run (capped at the stripe's first row and the borders)
+                const uint32_t v = (cx >> ((sh + (kk - (uint32_t)lane)) & 31u)) & 0x10001u;
+                const uint32_t run = min(streak_down(ballot(v == 0u), kk), min(min(i, j), r + 1u));
+                w.push('M', run);
+                i -= run;
+                j -= run;
             }
         } else if (state == 1) {
             w.push('I', 1);
@@ -617,9 +622,12 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
             if (has_next && (uint32_t)lane == nl - 1) B[j] = make_uint2(H2[R - 1], Flast);
         }
         if (CIGAR) {
-            const uint32_t off = t * kWave + (uint32_t)lane;
-            prow0[off] = make_uint2(__builtin_amdgcn_perm(ax0, ax1, 0x06020400u), __builtin_amdgcn_perm(ay0, ay1, 0x06020400u));
-            prow1[off] = make_uint2(__builtin_amdgcn_perm(ax0, ax1, 0x07030501u), __builtin_amdgcn_perm(ay0, ay1, 0x07030501u));
+            // 32-bit byte offset from the uniform row base (SGPR base + VGPR offset stores)
+            const uint32_t off = (t * kWave + (uint32_t)lane) * 8u;
+            *(uint2*)((char*)prow0 + off) =
+                make_uint2(__builtin_amdgcn_perm(ax0, ax1, 0x06020400u), __builtin_amdgcn_perm(ay0, ay1, 0x06020400u));
+            *(uint2*)((char*)prow1 + off) =
+                make_uint2(__builtin_amdgcn_perm(ax0, ax1, 0x07030501u), __builtin_amdgcn_perm(ay0, ay1, 0x07030501u));
         }
     };
     const uint32_t ramp_end = min(nl - 1, steps);
