@@ -542,6 +542,14 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
         t.slot_off = pl->d_slot_off;
         t.cigar_start = io->cigar_start;
         t.cigar_len = io->cigar_len;
+        t.score = io->score;
+        t.qbytes = reinterpret_cast<const uint8_t*>(io->query_bytes);
+        t.qoff = io->query_off;
+        t.tbytes = reinterpret_cast<const uint8_t*>(io->target_bytes);
+        t.toff = io->target_off;
+        t.match = pl->match;
+        t.mismatch = pl->mismatch;
+        t.gap = pl->gap;
         TA_HIP(pl->ctx, ta::launch_traceback(pl->type, t, s, tb_waves));
     }
     return TA_OK;

@@ -157,11 +157,35 @@ __device__ __forceinline__ uint32_t streak_down(uint64_t b, uint32_t from) {
     return (uint32_t)__clzll((long long)~(b << (63u - from)));  // shifted-in zeros stop the streak
 }
 
+// What the local walk needs besides the codes: the reference's loop runs
+// while the current cell's cost is > 0 (team_alignment.cpp:202).  The walk
+// tracks that cost exactly -- a cell with cost > 0 is unclamped, so its
+// parent's cost is its own minus the step's score (match_func / indel,
+// :20-28) -- instead of reading a STOP code, so the packed local fill need
+// not encode one.  Unused in global / semi-global walks.
+struct WalkSeq {
+    const uint8_t* Q;
+    const uint8_t* T;
+    int h;  // the goal cell's cost (the pair's score)
+    int ma, mi, gap;
+};
+
+// Lane L: bytes S[base-1-L] (bits 7:0) and S[base-65-L] (bits 15:8), zero below S[0].
+__device__ __forceinline__ uint32_t seq_window(const uint8_t* S, uint32_t base, int lane) {
+    const uint32_t L = (uint32_t)lane;
+    uint32_t v = 0;
+    if (L < base) v = S[base - 1 - L];
+    if (L + 64u < base) v |= (uint32_t)S[base - 65 - L] << 8;
+    return v;
+}
+
 template <int MODE>
 __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, uint32_t m, uint32_t gi, uint32_t gj,
                                                char* slot, uint64_t cap, int lane, uint64_t* start_in_slot,
-                                               uint32_t* len) {
+                                               uint32_t* len, const WalkSeq& seq) {
     RunWriter w{slot + cap, 0u, 0u, 0u, 0u, 0u, 0u, lane};
+    int H = seq.h;  // local: cost of the walk's current cell
+    uint32_t qbase = 0, tbase = 0, qw = 0, tw = 0;  // local: byte windows (seq_window)
     if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
         if (gi == n) {
             if (m - gj) w.push('I', m - gj);
@@ -179,7 +203,7 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
     uint32_t c0 = 0, c1 = 0, c2 = 0, c3 = 0, cur = 0;
     while (true) {
         if (MODE == kLocal) {
-            if (min(i, j) == 0) break;  // row/col 0 cost 0 ends the walk (:202)
+            if (H <= 0 || min(i, j) == 0) break;  // cost 0 ends the walk (:202); row/col 0 cost 0
         } else {
             if (i == 0) {  // row 0: INSERT parents (:89-92)
                 if (j) w.push('I', j);
@@ -189,6 +213,25 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
                 w.push('D', i);
                 break;
             }
+        }
+        // local: the bytes of the cells a run from here can cover (lane k: q[i-1-k],
+        // t[j-1-k]), from 128-byte windows refilled only after 64 rows / columns of
+        // progress, picked out with one ds_bpermute each
+        uint32_t qb = 0, tb = 0;
+        if (MODE == kLocal) {
+            if (i > qbase || qbase - i > 64u) {
+                qbase = i;
+                qw = seq_window(seq.Q, i, lane);
+            }
+            if (j > tbase || tbase - j > 64u) {
+                tbase = j;
+                tw = seq_window(seq.T, j, lane);
+            }
+            const uint32_t oq = qbase - i + (uint32_t)lane, ot = tbase - j + (uint32_t)lane;  // < 128
+            const uint32_t qv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((oq & 63u) << 2), (int)qw);
+            const uint32_t tv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ot & 63u) << 2), (int)tw);
+            qb = (qv >> ((oq >> 6) << 3)) & 0xFFu;
+            tb = (tv >> ((ot >> 6) << 3)) & 0xFFu;
         }
         const uint32_t row = i - 1;
         const uint32_t ln = (row >> 4) & 63u, r = row & 15u;
@@ -224,10 +267,11 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
         // step; M: step tt0+lane holds row r - (kk - lane), i.e. shift
         // sh + (kk - lane)) are both computed and picked with selects; hipcc
         // turns uniform if/else chains here into costly flag-register flow.
+        // D wins over I (the packed local fill stores raw compares; the int32
+        // fill's STOP code (D and I) only marks cost-0 cells, never reached here)
         const uint32_t dflag = (x >> 16) & 1u, iflag = x & 1u;
-        if (MODE == kLocal && (dflag & iflag)) break;  // STOP: cost == 0 (:202)
-        // D cells of rows r, r-1, .. (local: minus STOP cells): trailing ones
-        const uint32_t dp = (MODE == kLocal) ? ((x >> 16) & ~x) : (x >> 16);
+        // D cells of rows r, r-1, ..: trailing ones
+        const uint32_t dp = x >> 16;
         const uint32_t drun = (uint32_t)__builtin_ctz(~dp);  // <= r + 1
         const uint32_t lsh = sh + (kk - (uint32_t)lane) * (iflag ^ 1u);
         const uint32_t v = (cur >> (lsh & 31u)) & 0x10001u;
@@ -235,6 +279,50 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
         const uint32_t hrun = min(streak, iflag ? j : min(j, r + 1u));
         const uint32_t run = dflag ? drun : hrun;
         const uint32_t op = dflag ? 'D' : ('M' - 4u * iflag);
+        if (MODE == kLocal) {
+            // cost along the run: move k leaves cell c_k (lane k: row i-1-k / column j-1-k
+            // bytes, loaded at the top of the iteration); the walk stops at the first c_k
+            // (k >= 1) whose cost is 0.  A run can reach 0 only if H <= run * (largest
+            // positive step score); otherwise the cost just moves by the run's total.
+            const bool in = (uint32_t)lane < run;
+            int d;
+            int pos;  // largest positive step score of this run kind
+            if (op == 'M') {
+                d = (qb == tb) ? seq.ma : seq.mi;
+                pos = max(0, max(seq.ma, seq.mi));
+            } else {
+                const uint32_t c = (op == 'D') ? qb : tb;
+                d = (c == '-') ? 0 : seq.gap;
+                pos = max(0, seq.gap);
+            }
+            uint32_t emit = run;
+            bool stop = false;
+            if (H > (int)run * pos) {
+                // total = sum of d over the run: two score values, counted with one ballot
+                const int d0 = (op == 'M') ? seq.ma : 0, d1 = (op == 'M') ? seq.mi : seq.gap;
+                const uint32_t c0 = (uint32_t)__builtin_popcountll(ballot(in && d == d0 && d0 != d1));
+                H -= (d0 == d1) ? (int)run * d0 : (int)c0 * d0 + (int)(run - c0) * d1;
+            } else {
+                int incl = in ? d : 0;  // inclusive prefix over the run's cells
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const int v = __shfl_up(incl, o, 64);
+                    if (lane >= o) incl += v;
+                }
+                const uint64_t z = ballot(in && H - incl <= 0);
+                if (z) {
+                    emit = (uint32_t)__builtin_ctzll(z) + 1u;
+                    stop = true;
+                } else {
+                    H -= rdlane(incl, run - 1u);
+                }
+            }
+            w.push(op, emit);
+            i -= (op == 'I') ? 0u : emit;
+            j -= dflag ? 0u : emit;
+            if (stop) break;
+            continue;
+        }
         w.push(op, run);
         i -= (op == 'I') ? 0u : run;
         j -= dflag ? 0u : run;

@@ -18,6 +18,8 @@
 // pairs to bytes and v_bfi_b32 inserts them into two row-group accumulators,
 // which two more v_perm_b32 per step turn into the per-pair bit-plane dwords
 // of ta_internal.h (Code).  No lane masks, no SALU, no v_addc chains.
+// Local mode stores the raw compares too (no STOP code): the local walk
+// tracks the cell cost and stops where it reaches 0 (ta_device.h WalkSeq).
 #include "ta_device.h"
 #include "ta_packed.h"
 
@@ -158,14 +160,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 const uint32_t u = pk_max(m1, up);
                 const uint32_t hv = LOCAL ? pk_max(u, Z) : u;  // clamp, :185
                 if (CIGAR) {
-                    uint32_t wd = pk_sub_sat(m1, up);    // sign: up > max(diag, left)  (DELETE)
-                    uint32_t wi = pk_sub_sat(diag, left);  // sign: left > diag           (INSERT)
-                    if (LOCAL) {
-                        // canonical codes: D | S and (I & !D) | S, S = clamped to 0
-                        const uint32_t wn = pk_sub_sat(Z, u);  // sign: u > 0 (not STOP)
-                        wi = (wi & ~wd) | ~wn;
-                        wd = wd | ~wn;
-                    }
+                    // raw compares (D wins over I in the walk; local walks track the
+                    // cost instead of reading a STOP code, ta_device.h WalkSeq)
+                    const uint32_t wd = pk_sub_sat(m1, up);    // sign: up > max(diag, left)  (DELETE)
+                    const uint32_t wi = pk_sub_sat(diag, left);  // sign: left > diag           (INSERT)
                     uint32_t& acc = (r < 8) ? acc0 : acc1;
                     acc = bfi(0x01010101u << (7 - (r & 7)), sign_bytes(wd, wi), acc);
                 }
@@ -359,8 +357,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
         if (CIGAR && a.fused) {
             uint64_t st;
             uint32_t len;
+            const WalkSeq seq{io.Q[h], io.T[h], best_h[h], a.match, a.mismatch, a.gap};
             traceback_pair<MODE>(io.ptrs[h], n, m, gi, gj, a.slots + a.slot_off[p[h]], cigar_slot_bytes(n, m), lane,
-                                 &st, &len);
+                                 &st, &len, seq);
             if (lane == 0) {
                 a.cigar_start[p[h]] = a.slot_off[p[h]] + st;
                 a.cigar_len[p[h]] = len;

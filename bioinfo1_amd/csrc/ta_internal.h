@@ -94,6 +94,13 @@ struct TraceArgs {
     const uint64_t* slot_off;
     uint64_t* cigar_start;
     uint32_t* cigar_len;
+    // local walks track the cost (ta_device.h WalkSeq)
+    const int32_t* score;
+    const uint8_t* qbytes;
+    const uint64_t* qoff;
+    const uint8_t* tbytes;
+    const uint64_t* toff;
+    int match, mismatch, gap;
 };
 
 struct CompactArgs {

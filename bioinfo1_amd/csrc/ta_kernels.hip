@@ -34,10 +34,11 @@ namespace {
 #ifdef TA_FILL_MODE
 template <int MODE>
 __device__ __forceinline__ void fused_traceback(const FillArgs& a, uint32_t p, const uint32_t* ptrs, uint32_t n,
-                                                uint32_t m, uint32_t gi, uint32_t gj, int lane) {
+                                                uint32_t m, uint32_t gi, uint32_t gj, int lane, int h) {
     uint64_t st;
     uint32_t len;
-    traceback_pair<MODE>(ptrs, n, m, gi, gj, a.slots + a.slot_off[p], cigar_slot_bytes(n, m), lane, &st, &len);
+    const WalkSeq seq{a.qbytes + a.qoff[p], a.tbytes + a.toff[p], h, a.match, a.mismatch, a.gap};
+    traceback_pair<MODE>(ptrs, n, m, gi, gj, a.slots + a.slot_off[p], cigar_slot_bytes(n, m), lane, &st, &len, seq);
     if (lane == 0) {
         a.cigar_start[p] = a.slot_off[p] + st;
         a.cigar_len[p] = len;
@@ -337,7 +338,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
         if (CIGAR && a.fused) {
             // no cells: the walk is the closed-form boundary run (global/semi) or "1\0"
             const uint32_t gi = (MODE == kGlobal) ? n : 0, gj = (MODE == kGlobal || n == 0) ? m : 0;
-            fused_traceback<MODE>(a, p, nullptr, n, m, MODE == kLocal ? 0 : gi, MODE == kLocal ? 0 : gj, lane);
+            fused_traceback<MODE>(a, p, nullptr, n, m, MODE == kLocal ? 0 : gi, MODE == kLocal ? 0 : gj, lane, 0);
         }
         return;
     }
@@ -373,7 +374,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
         fused_traceback<MODE>(a, p, ptrs, n, m, (MODE == kGlobal) ? n : best_i, (MODE == kGlobal) ? m : best_j,
-                              lane);
+                              lane, best_h);
     }
     if (lane == 0) {
         a.score[p] = (MODE == kGlobal) ? corner : best_h;
@@ -399,8 +400,10 @@ __global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
         const uint32_t n = a.qlen[p], m = a.tlen[p];
         uint64_t st;
         uint32_t len;
+        const WalkSeq seq{a.qbytes + a.qoff[p], a.tbytes + a.toff[p], MODE == kLocal ? a.score[p] : 0, a.match,
+                          a.mismatch, a.gap};
         traceback_pair<MODE>(a.ptrs + a.ptr_off[p], n, m, a.goal_i[p], a.goal_j[p], a.slots + a.slot_off[p],
-                             cigar_slot_bytes(n, m), lane, &st, &len);
+                             cigar_slot_bytes(n, m), lane, &st, &len, seq);
         if (lane == 0) {
             a.cigar_start[p] = a.slot_off[p] + st;
             a.cigar_len[p] = len;

@@ -47,8 +47,7 @@ __device__ __forceinline__ uint32_t pk_sub_sat(uint32_t a, uint32_t b) {
 // spread to whole bytes by v_perm_b32 (selectors 8..11 replicate the sign of
 // bytes 1, 3, 5, 7), giving [I_A, I_B, D_A, D_B] as 0x00/0xFF bytes, and one
 // bit-insert (v_bitop3_b32 on gfx950) drops them into bit (7 - r%8) of the
-// row group's accumulator.  The local-mode canonicalisation is two more
-// v_bitop3_b32, which hipcc forms from the logic expressions.
+// row group's accumulator.
 constexpr uint32_t kSignBytes = 0x0B0A0908u;
 __device__ __forceinline__ uint32_t sign_bytes(uint32_t dword_d, uint32_t dword_i) {
     return __builtin_amdgcn_perm(dword_d, dword_i, kSignBytes);
