@@ -186,6 +186,16 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
     RunWriter w{slot + cap, 0u, 0u, 0u, 0u, 0u, 0u, lane};
     int H = seq.h;  // local: cost of the walk's current cell
     uint32_t qbase = 0, tbase = 0, qw = 0, tw = 0;  // local: byte windows (seq_window)
+    // local: gap runs need no bytes when their sequence has no '-' and gap <= 0
+    bool gfastD = false, gfastI = false;
+    const int posM = max(0, max(seq.ma, seq.mi));
+    if (MODE == kLocal) {
+        bool a = false, b = false;
+        for (uint32_t k = (uint32_t)lane; k < n; k += 64) a |= seq.Q[k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < m; k += 64) b |= seq.T[k] == '-';
+        gfastD = ballot(a) == 0 && seq.gap <= 0;
+        gfastI = ballot(b) == 0 && seq.gap <= 0;
+    }
     if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
         if (gi == n) {
             if (m - gj) w.push('I', m - gj);
@@ -281,28 +291,22 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
         const uint32_t op = dflag ? 'D' : ('M' - 4u * iflag);
         if (MODE == kLocal) {
             // cost along the run: move k leaves cell c_k (lane k: row i-1-k / column j-1-k
-            // bytes, loaded at the top of the iteration); the walk stops at the first c_k
-            // (k >= 1) whose cost is 0.  A run can reach 0 only if H <= run * (largest
-            // positive step score); otherwise the cost just moves by the run's total.
-            const bool in = (uint32_t)lane < run;
-            int d;
-            int pos;  // largest positive step score of this run kind
-            if (op == 'M') {
-                d = (qb == tb) ? seq.ma : seq.mi;
-                pos = max(0, max(seq.ma, seq.mi));
-            } else {
-                const uint32_t c = (op == 'D') ? qb : tb;
-                d = (c == '-') ? 0 : seq.gap;
-                pos = max(0, seq.gap);
-            }
+            // bytes); the walk stops at the first c_k (k >= 1) whose cost is 0.  A run can
+            // reach 0 only if H <= run * (largest positive step score); otherwise the cost
+            // just moves by the run's total.
             uint32_t emit = run;
             bool stop = false;
-            if (H > (int)run * pos) {
-                // total = sum of d over the run: two score values, counted with one ballot
-                const int d0 = (op == 'M') ? seq.ma : 0, d1 = (op == 'M') ? seq.mi : seq.gap;
-                const uint32_t c0 = (uint32_t)__builtin_popcountll(ballot(in && d == d0 && d0 != d1));
-                H -= (d0 == d1) ? (int)run * d0 : (int)c0 * d0 + (int)(run - c0) * d1;
+            const uint64_t inrun = run >= 64u ? ~0ull : ((1ull << run) - 1ull);
+            if (op == 'M' && H > (int)run * posM) {
+                const int c = __builtin_popcountll(ballot(qb == tb) & inrun);  // matches
+                H -= c * seq.ma + ((int)run - c) * seq.mi;
+            } else if (op != 'M' && (op == 'D' ? gfastD : gfastI)) {
+                H -= (int)run * seq.gap;  // uniform gap steps (gap <= 0) never lower the cost
             } else {
+                const bool in = (uint32_t)lane < run;
+                int d;
+                if (op == 'M') d = (qb == tb) ? seq.ma : seq.mi;
+                else d = (((op == 'D') ? qb : tb) == '-') ? 0 : seq.gap;
                 int incl = in ? d : 0;  // inclusive prefix over the run's cells
 #pragma unroll
                 for (int o = 1; o < 64; o <<= 1) {
