@@ -195,6 +195,10 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
         for (uint32_t k = (uint32_t)lane; k < m; k += 64) b |= seq.T[k] == '-';
         gfastD = ballot(a) == 0 && seq.gap <= 0;
         gfastI = ballot(b) == 0 && seq.gap <= 0;
+        qbase = gi;  // the walk only moves up / left: windows below the goal
+        tbase = gj;
+        qw = seq_window(seq.Q, gi, lane);
+        tw = seq_window(seq.T, gj, lane);
     }
     if (MODE == kSemi && (gj != m || gi != n)) {  // :306-315
         if (gi == n) {
@@ -223,25 +227,6 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
                 w.push('D', i);
                 break;
             }
-        }
-        // local: the bytes of the cells a run from here can cover (lane k: q[i-1-k],
-        // t[j-1-k]), from 128-byte windows refilled only after 64 rows / columns of
-        // progress, picked out with one ds_bpermute each
-        uint32_t qb = 0, tb = 0;
-        if (MODE == kLocal) {
-            if (i > qbase || qbase - i > 64u) {
-                qbase = i;
-                qw = seq_window(seq.Q, i, lane);
-            }
-            if (j > tbase || tbase - j > 64u) {
-                tbase = j;
-                tw = seq_window(seq.T, j, lane);
-            }
-            const uint32_t oq = qbase - i + (uint32_t)lane, ot = tbase - j + (uint32_t)lane;  // < 128
-            const uint32_t qv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((oq & 63u) << 2), (int)qw);
-            const uint32_t tv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ot & 63u) << 2), (int)tw);
-            qb = (qv >> ((oq >> 6) << 3)) & 0xFFu;
-            tb = (tv >> ((ot >> 6) << 3)) & 0xFFu;
         }
         const uint32_t row = i - 1;
         const uint32_t ln = (row >> 4) & 63u, r = row & 15u;
@@ -296,12 +281,31 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
             // just moves by the run's total.
             uint32_t emit = run;
             bool stop = false;
+            const bool gfast = op != 'M' && (op == 'D' ? gfastD : gfastI);
+            // the bytes of the run's cells (lane k: q[i-1-k], t[j-1-k]) from 128-byte
+            // windows refilled only after 64 rows / columns of progress, one ds_bpermute each
+            uint32_t qb = 0, tb = 0;
+            if (!gfast) {
+                if (qbase - i > 64u) {
+                    qbase = i;
+                    qw = seq_window(seq.Q, i, lane);
+                }
+                if (tbase - j > 64u) {
+                    tbase = j;
+                    tw = seq_window(seq.T, j, lane);
+                }
+                const uint32_t oq = qbase - i + (uint32_t)lane, ot = tbase - j + (uint32_t)lane;  // < 128
+                const uint32_t qv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((oq & 63u) << 2), (int)qw);
+                const uint32_t tv = (uint32_t)__builtin_amdgcn_ds_bpermute((int)((ot & 63u) << 2), (int)tw);
+                qb = (qv >> ((oq >> 6) << 3)) & 0xFFu;
+                tb = (tv >> ((ot >> 6) << 3)) & 0xFFu;
+            }
             const uint64_t inrun = run >= 64u ? ~0ull : ((1ull << run) - 1ull);
-            if (op == 'M' && H > (int)run * posM) {
+            if (gfast) {
+                H -= (int)run * seq.gap;  // uniform gap steps (gap <= 0) never lower the cost
+            } else if (op == 'M' && H > (int)run * posM) {
                 const int c = __builtin_popcountll(ballot(qb == tb) & inrun);  // matches
                 H -= c * seq.ma + ((int)run - c) * seq.mi;
-            } else if (op != 'M' && (op == 'D' ? gfastD : gfastI)) {
-                H -= (int)run * seq.gap;  // uniform gap steps (gap <= 0) never lower the cost
             } else {
                 const bool in = (uint32_t)lane < run;
                 int d;
