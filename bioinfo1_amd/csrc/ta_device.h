@@ -191,8 +191,15 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
     const int posM = max(0, max(seq.ma, seq.mi));
     if (MODE == kLocal) {
         bool a = false, b = false;
-        for (uint32_t k = (uint32_t)lane; k < n; k += 64) a |= seq.Q[k] == '-';
-        for (uint32_t k = (uint32_t)lane; k < m; k += 64) b |= seq.T[k] == '-';
+        const uint32_t nm = max(n, m);
+        for (uint32_t k0 = (uint32_t)lane; k0 < nm; k0 += 256) {  // 8 loads in flight per wait
+#pragma unroll
+            for (uint32_t u = 0; u < 4; ++u) {
+                const uint32_t k = k0 + 64u * u;
+                a |= k < n && seq.Q[k] == '-';
+                b |= k < m && seq.T[k] == '-';
+            }
+        }
         gfastD = ballot(a) == 0 && seq.gap <= 0;
         gfastI = ballot(b) == 0 && seq.gap <= 0;
         qbase = gi;  // the walk only moves up / left: windows below the goal
