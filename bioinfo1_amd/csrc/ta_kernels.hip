@@ -388,7 +388,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
 
 #ifdef TA_TU_MISC
 template <int MODE>
-__global__ __launch_bounds__(kBlock) void traceback_kernel(TraceArgs a) {
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void traceback_kernel(TraceArgs a) {
     // Wave-strided over the pairs: one wave per pair when the grid covers
     // them all, fewer resident waves (each walking several pairs) when the
     // launch is capped so it fits beside the next batch's fill (see
