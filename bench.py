@@ -95,7 +95,9 @@ def parse():
         a.mode = a.mode or "semiGlobal"
         a.cpu_pairs = min(a.cpu_pairs, 200)
     else:
-        a.pairs = a.pairs or 2000
+        # a slice of config 5's 100k pairs that fills the GPU in one chunk: 8,192 pairs (4,096
+        # two-pair waves, 197 GB of 2-bit codes); affine 4,096 (4-bit codes, 197 GB)
+        a.pairs = a.pairs or (8192 if a.gap_open is None else 4096)
         a.mode = a.mode or "semiGlobal"
         a.qlen = a.tlen = 10000
         a.related = True
