@@ -202,7 +202,7 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
         }
         gfastD = ballot(a) == 0 && seq.gap <= 0;
         gfastI = ballot(b) == 0 && seq.gap <= 0;
-        qbase = gi;  // the walk only moves up / left: windows below the goal
+        qbase = gi;  // the walk only moves up / left: windows end at the goal cell
         tbase = gj;
         qw = seq_window(seq.Q, gi, lane);
         tw = seq_window(seq.T, gj, lane);
