@@ -372,3 +372,29 @@ def test_flex_records_ignore_stale_workspace():
                 np.testing.assert_array_equal(r.cigar_lens, d["cigar_lens"])
     finally:
         al.close()
+
+
+@pytest.mark.parametrize("sc", [(2, -1, 1), (1, -1, -1), (3, -2, 0), (1, 2, -3)])
+def test_local_walk_cost_tracking(aligner, oracle, sc):
+    """Packed local fill (raw codes, no STOP) + the cost-tracking walk: '-'
+    only in targets (the couples stay packed), gap > 0 / = 0 / < 0, mismatch
+    above match: every stop rule of the walk (closed-form gap runs, byte
+    windows, prefix-sum stop inside a run) against the oracle."""
+    rng = np.random.default_rng(0x10CA1 + sc[0] * 7 + sc[2])
+    qa, ta = np.frombuffer(b"ACGT", np.uint8), np.frombuffer(b"ACGT-", np.uint8)
+    shapes = [(300, 280), (64, 64), (1030, 900), (17, 130)]
+    pairs = []
+    for k in range(64):
+        n, m = shapes[k % len(shapes)]
+        pairs.append((qa[rng.integers(4, size=n)].tobytes(), ta[rng.integers(5, size=m)].tobytes()))
+    b = synth.from_pairs(pairs)
+    plan = DevicePlan(aligner, b, 1, *sc, True)
+    # 1030 x 900 leaves int16 for gap > 0 or match 3 (fits_int16): those couples run int32
+    assert plan.dual_pairs >= 48, plan.dual_pairs
+    plan.close()
+    want = oracle.align_batch(b, 1, *sc, True)
+    got = aligner.align_batch(b, 1, *sc, True)
+    np.testing.assert_array_equal(got.scores, want.scores)
+    np.testing.assert_array_equal(got.target_begins, want.target_begins)
+    for p in range(b.n_pairs):
+        assert got.cigar(p) == want.cigar(p), (sc, p)
