@@ -127,11 +127,11 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         tcur[h] = load_tchunk(io.T[h], io.m[h], 0, lane);
         tnext[h] = load_tchunk(io.T[h], io.m[h], 1, lane);
     }
-    int bcur[2] = {0, 0}, bnext[2] = {0, 0};
-    if (pass > 0) {
-        load_rec_chunk(io, M, 0, lane, bcur);
-        load_rec_chunk(io, M, 1, lane, bnext);
-    }
+    // the previous pass's bottom row, polled one 64-column chunk at a time just
+    // before it is needed (no prefetch of the next chunk: that would make every
+    // pass trail its predecessor by one more chunk)
+    int bcur[2] = {0, 0};
+    if (pass > 0) load_rec_chunk(io, M, 0, lane, bcur);
     const uint32_t steps = M + nl - 1;
     const uint32_t Tmax0 = pass_steps(io.m[0]), Tmax1 = pass_steps(io.m[1]);
     uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * Tmax0 * kWave : nullptr;
@@ -146,9 +146,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             }
         }
         if (pass > 0) {
-            bcur[0] = bnext[0];
-            bcur[1] = bnext[1];
-            load_rec_chunk(io, M, (t >> 6) + 1, lane, bnext);
+            load_rec_chunk(io, M, t >> 6, lane, bcur);
         }
         // rebase (every 64 steps, all lanes alike): a lane that holds current cells
         const uint32_t d = (uint32_t)rdlane((int)H2[0], t < M ? 0u : nl - 1);
