@@ -31,6 +31,9 @@ struct ta_plan {
     bool staged = false;  // chunks use disjoint workspace: traceback k overlaps fill k+1
     std::vector<uint32_t> qlen, tlen, order, singles, duals, flexes;
     std::vector<uint32_t> flex_task_off;  // per flex couple: first task (one per query pass); + total
+    // per chunk, the chunk's tasks in ticket order: pass-major (every couple's pass 0, then every
+    // pass 1, ...), so a pass starts long after its predecessor instead of trailing it by a chunk
+    std::vector<uint32_t> flex_tasks;
     std::vector<uint64_t> slot_off;
     struct Chunk {
         uint32_t begin, count;    // all pairs (traceback order)
@@ -49,7 +52,7 @@ struct ta_plan {
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
     uint32_t *d_goal_i = nullptr, *d_goal_j = nullptr;
     uint32_t* d_fb = nullptr;  // dual fallback: [n_dual_pairs] list, then one counter per chunk
-    uint32_t *d_flex_task_off = nullptr, *d_tickets = nullptr, *d_err = nullptr;
+    uint32_t *d_flex_task_off = nullptr, *d_tickets = nullptr, *d_err = nullptr, *d_flex_tasks = nullptr;
     void* d_pout = nullptr;  // PassOut[2] per flex task
 };
 
@@ -175,7 +178,8 @@ void ta_plan_destroy(ta_plan* pl) {
     (void)hipSetDevice(pl->ctx->device);
     for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_flexes, (void*)pl->d_ptr_off,
                     (void*)pl->d_bnd_off, (void*)pl->d_slot_off, (void*)pl->d_goal_i, (void*)pl->d_goal_j,
-                    (void*)pl->d_fb, (void*)pl->d_flex_task_off, (void*)pl->d_tickets, (void*)pl->d_err, pl->d_pout})
+                    (void*)pl->d_fb, (void*)pl->d_flex_task_off, (void*)pl->d_tickets, (void*)pl->d_err, pl->d_pout,
+                    (void*)pl->d_flex_tasks})
         if (p) (void)hipFree(p);
     delete pl;
 }
@@ -361,6 +365,15 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     pl->flex_task_off.assign(1, 0);
     for (size_t w = 0; w < pl->flexes.size() / 2; ++w)
         pl->flex_task_off.push_back(pl->flex_task_off.back() + ta::n_passes(pl->qlen[pl->flexes[2 * w]]));
+    pl->flex_tasks.assign(pl->flex_task_off.back(), 0u);
+    for (const auto& ch : pl->chunks) {
+        uint32_t at = pl->flex_task_off[ch.fbegin], maxp = 0;
+        for (uint32_t w = ch.fbegin; w < ch.fbegin + ch.fcount; ++w)
+            maxp = std::max(maxp, pl->flex_task_off[w + 1] - pl->flex_task_off[w]);
+        for (uint32_t ps = 0; ps < maxp; ++ps)
+            for (uint32_t w = ch.fbegin; w < ch.fbegin + ch.fcount; ++w)
+                if (pl->flex_task_off[w + 1] - pl->flex_task_off[w] > ps) pl->flex_tasks[at++] = w * 64u + ps;
+    }
     if (pl->staged) {
         pl->ws_ptr_dwords = off_pd;
         pl->ws_bnd_words = off_bw;
@@ -382,6 +395,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     up(upload(ctx, &pl->d_flexes, pl->flexes));
     if (!pl->flexes.empty()) {
         up(upload(ctx, &pl->d_flex_task_off, pl->flex_task_off));
+        up(upload(ctx, &pl->d_flex_tasks, pl->flex_tasks));
         up(upload(ctx, &pl->d_tickets, std::vector<uint32_t>(pl->chunks.size(), 0u)));
         up(upload(ctx, &pl->d_err, std::vector<uint32_t>(1, 0u)));
         if (rc == TA_OK && hipMalloc(&pl->d_pout, pl->flex_task_off.back() * 48ull + 16) != hipSuccess)
@@ -504,6 +518,7 @@ static int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32
                 d.fb_list = fb_list;
                 d.fb_count = fb_count;
                 d.task_off = pl->d_flex_task_off;
+                d.tasks = pl->d_flex_tasks;
                 d.ticket = pl->d_tickets + c;
                 d.n_tasks = pl->flex_task_off[ch.fbegin + ch.fcount] - pl->flex_task_off[ch.fbegin];
                 d.epoch = ++ctx->epoch & 0x3FFFFFFu;

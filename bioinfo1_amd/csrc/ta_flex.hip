@@ -317,9 +317,12 @@ constexpr uint32_t kSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to the 
 
 // One wave per (couple, pass).  flex order: 2 pair ids per couple, pair A
 // (larger n) first; same pass count and n mod 16 (a single long pair may be
-// coupled with itself).  A wave takes the next ticket; tasks are numbered
-// couple by couple, pass by pass, so pass p-1 of its couple belongs to a wave
-// that took an earlier ticket and is running: every poll ends.
+// coupled with itself).  A wave takes the next ticket; the chunk's tasks are
+// in pass-major order (every couple's pass 0, then every pass 1, ...; the host's
+// flex_tasks), so pass p-1 of its couple belongs to a wave that took an earlier
+// ticket and is running: every poll ends.  Pass-major also means a pass starts
+// long after its predecessor, instead of all passes of a couple starting
+// together and each waiting for the one above.
 template <int MODE, bool CIGAR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_WAVES))) void flex_fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
@@ -327,14 +330,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
     if (lane == 0) tk = atomicAdd(a.ticket, 1u);
     tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
     if (tk >= a.n_tasks) return;
-    const uint32_t g = a.task_off[a.begin] + tk;  // plan-global task index
-    uint32_t lo = a.begin, hi = a.begin + a.count;  // couple: last w with task_off[w] <= g
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (a.task_off[mid] <= g) lo = mid;
-        else hi = mid;
-    }
-    const uint32_t w = lo, pass = g - a.task_off[w];
+    const uint32_t code = a.tasks[a.task_off[a.begin] + tk];  // this chunk's tasks, pass-major
+    const uint32_t w = code >> 6, pass = code & 63u;
+    const uint32_t g = a.task_off[w] + pass;  // plan-global task index (couple-major): its PassOut
     uint32_t p[2];
     p[0] = a.order[2 * w];
     p[1] = a.order[2 * w + 1];

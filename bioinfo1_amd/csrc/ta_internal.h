@@ -74,6 +74,7 @@ struct FillArgs {
     // flexible fill, one wave per (couple, pass): waves take tickets in launch
     // order, so every pass a wave waits on is already held by a running wave
     const uint32_t* task_off;  // per flex couple (plan order): its first task; [w + 1] - [w] = passes
+    const uint32_t* tasks;     // ticket order: couple * 64 + pass, pass-major within a chunk
     uint32_t* ticket;          // this launch's ticket counter (zeroed before the launch)
     uint32_t n_tasks;          // tasks of this launch
     uint32_t epoch;            // tag base of this launch's pass hand-off records
