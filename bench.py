@@ -9,7 +9,8 @@ CIGAR) left in HBM.  With N GPUs (torch.distributed.run, one process per
 GPU, RCCL) every rank aligns its own 10,000 pairs (weak scaling: pairs are
 independent, the batch is range-split by pair index) and the fixed-size
 per-pair records of every step are all-gathered over RCCL inside the timed
-region.  --pipeline runs the K steps as one pipelined sequence of K batches
+region (asynchronously: step k's gather overlaps step k+1; drained before
+the clock stops).  --pipeline runs the K steps as one pipelined sequence of K batches
 (ta_plan_execute_batches: batch k's traceback beside batch k+1's fill, each
 batch with its own outputs).  batch_latency_ms = one batch alone (fill +
 traceback kernels, HIP events).
@@ -391,7 +392,15 @@ def main():
                 rec[k, 2].copy_(o.cigar_len if cigar else o.score)
             rec = rec.to(coll_dev)
             out = torch.empty((world * len(sets), 3, P), dtype=torch.int32, device=coll_dev)
-            dist.all_gather_into_tensor(out, rec)
+            # asynchronous: step k's gather overlaps step k+1's kernels; drained before the clock stops
+            pending.append((rec, out, dist.all_gather_into_tensor(out, rec, async_op=True)))
+
+    pending = []
+
+    def drain():
+        for _, _, h in pending:
+            h.wait()
+        pending.clear()
 
     def run_steps(k):
         if k <= 0:
@@ -405,10 +414,12 @@ def main():
                 gather([plan])
 
     run_steps(args.warmup)
+    drain()
     parity = None
     if rank == 0 and not args.no_parity:
         if args.warmup < (2 if pipelined else 1):
-            run_steps(2 if pipelined else 1)
+            # compute only (rank 0 alone: no collective here)
+            plan.run_batches(outs[:2]) if pipelined else plan.run()
         parity = parity_vs_digest(plan.results(), batch, args)
         if parity is not None and pipelined:  # batch 1 ran beside batch 0 (capped traceback grid on its own)
             p1 = parity_vs_digest(outs[1].results(), batch, args)
@@ -424,6 +435,7 @@ def main():
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     run_steps(args.steps)
+    drain()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
