@@ -1,42 +1,51 @@
 #!/usr/bin/env python3
-"""Benchmark of the team::Align hot path on MI355X (BASELINE.json config 2).
+"""Benchmark of the team::Align hot path on MI355X (BASELINE.json).
 
-One "step" = one pass of the path over one batch: the DP fill kernel and the
-traceback/CIGAR kernel for 10,000 synthetic 1 kb x 1 kb read-vs-window pairs,
-Smith-Waterman (local), match/mismatch/gap = 1/-1/-1, CIGAR on -- inputs
-resident in HBM before the timed region, results (score, target_begin,
-CIGAR) left in HBM.  With N GPUs (torch.distributed.run, one process per
-GPU, RCCL) every rank aligns its own 10,000 pairs (weak scaling: pairs are
-independent, the batch is range-split by pair index) and the fixed-size
-per-pair records of every step are all-gathered over RCCL inside the timed
-region (asynchronously: step k's gather overlaps step k+1; drained before
-the clock stops).  --pipeline runs the K steps as one pipelined sequence of K batches
-(ta_plan_execute_batches: batch k's traceback beside batch k+1's fill, each
-batch with its own outputs).  batch_latency_ms = one batch alone (fill +
-traceback kernels, HIP events).
+Default workload = BASELINE config 2: one "step" is one pass of the path over
+one batch -- the DP fill kernels and the traceback/CIGAR kernel for 10,000
+synthetic 1 kb x 1 kb read-vs-window pairs per GPU, Smith-Waterman (local),
+match/mismatch/gap = 1/-1/-1, CIGAR on -- with the inputs resident in HBM
+before the timed region.
 
-Prints ONE JSON line (rank 0).  value = whole-job GCUPS = (sum of n*m over
-all ranks' pairs) / (max over ranks of the step time).
+Multi-GPU: one process per GPU.  `--gpus N` without a
+torch.distributed environment starts the N ranks itself (torch.distributed.run
+as a child process, before this process touches the GPU) and exits with its
+status; every rank checks WORLD_SIZE == --gpus.  Config 2 is weak-scaled (each
+rank aligns its own 10,000-pair range of the seeded stream); config 4
+(`--workload cfg4`) strong-scales one fixed read set (the config-3 stand-in)
+range-split by cells (bioinfo1_amd/shard.py).  In every step each rank's
+results -- the fixed per-pair records (score, target_begin, cigar_len) and the
+CIGAR bytes, compacted on the device -- are all-gathered over RCCL inside the
+timed region: the records of step k right after its kernels, its CIGAR bytes
+(whose sizes the records carry) once step k+1 is enqueued, so neither stalls
+the GPU; all gathers are drained before the clock stops.  value = total cells
+of all ranks / max over ranks of the step time.
 
-Also reported, on rank 0:
-  roofline      -- the fill kernel's algorithmic bytes per launch / its
-                   average duration (HIP events on the launch stream) against
-                   the 8 TB/s HBM peak; traffic = PMC-measured HBM bytes per
-                   launch from profiles/ when present.
-  valu          -- the same kernel against the VALU int32 roofline (the roof
-                   that actually binds this integer DP).
+Also reported (rank 0):
+  roofline      -- the dominant fill kernel: algorithmic bytes per launch /
+                   its HIP-event duration on its launch stream, against the
+                   8 TB/s HBM peak; traffic = rocprofv3 PMC HBM bytes per launch
+                   of this same command (profiles/traffic.json, collected by
+                   scripts/profile.sh; rocprof counters cannot be read in-process).
+  valu          -- the same kernel against the VALU int32 issue roof (the roof
+                   that binds this integer DP; ops/cell from profiles/valu.json).
+  host_to_host  -- the same batch through ta_align_batch from pinned host memory
+                   to host results (PCIe both ways), SURVEY §8d's GCUPS definition.
   cpu_baseline  -- the reference team::Align (oracle/_ref, compiled from the
-                   reference sources) or, where it was not built, our C
-                   restatement (oracle/), on the node's host cores, OpenMP
-                   over pairs, on a bounded sample of the same batch.
-  parity        -- this run's first step compared with the committed golden
-                   digest of the same seeded batch (tests/golden/).
+                   reference sources), OpenMP over pairs on the box's host cores,
+                   plus a 1-thread figure, on bounded samples of the same batch.
+  parity        -- results against the committed golden digest made by the
+                   reference (tests/golden/), the CPU oracle, or (config 4) the
+                   1-GPU result of the same read set.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -44,58 +53,61 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 import numpy as np  # noqa: E402
-import torch  # noqa: E402
-
-from bioinfo1_amd import synth  # noqa: E402
-from bioinfo1_amd.align import Aligner, DevicePlan  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, Chip-level parameters)
 # int32 VALU: a wave64 integer instruction occupies its SIMD for 4 cycles (measured:
 # SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU quad-cycles at ~100% busy), i.e. 16 lanes/clk/SIMD:
 # 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T lane-ops/s
 VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; bit-exact score+CIGAR"
+MODES = {"global": 0, "local": 1, "semiGlobal": 2}
+DTYPE = "int32 semantics; packed int16 arithmetic where range-proven (fits_int16), else int32"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg5", "cfg3map"],
+    ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "cfg3map", "dropin"],
                     help="cfg2: 1kx1k pairs (headline); cfg3: E. coli stand-in, ONT-like reads vs true-origin "
-                         "windows, semiGlobal; cfg5: 10kx10k related semiGlobal (a sample of the 100k pairs); "
-                         "cfg3map: config 3 end to end -- minimizer seeding, FindLIS chaining and semiGlobal "
-                         "alignment of the same reads against the 4.64 Mb genome (team_mapper pipeline)")
-    ap.add_argument("--pairs", type=int, default=0, help="pairs per GPU (0 = the workload's default)")
+                         "windows, semiGlobal, per GPU; cfg4: ONE such read set range-split by cells over the GPUs "
+                         "(strong scaling); cfg5: 10kx10k related semiGlobal pairs (--pairs 100000 = the stated "
+                         "size, generated in HBM); cfg3map: config 3 end to end (minimizers, FindLIS, alignment); "
+                         "dropin: single-call team::Align latency/throughput vs the reference Align")
+    ap.add_argument("--pairs", type=int, default=0, help="pairs per GPU (cfg4: in total; 0 = the workload's default)")
     ap.add_argument("--qlen", type=int, default=1000)
     ap.add_argument("--tlen", type=int, default=1000)
     ap.add_argument("--mode", default=None, choices=["global", "local", "semiGlobal"])
     ap.add_argument("--scoring", default="1,-1,-1")
     ap.add_argument("--related", action="store_true", help="config-2 related variant (5%% sub/ins/del)")
     ap.add_argument("--no-cigar", action="store_true", help="score-only (cigar == nullptr) mode")
-    ap.add_argument("--cpu-pairs", type=int, default=10000, help="CPU-baseline sample size (pairs)")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+    ap.add_argument("--cpu-pairs", type=int, default=10000, help="CPU-baseline sample size (pairs), all threads")
+    ap.add_argument("--cpu-pairs-1t", type=int, default=400, help="CPU-baseline sample size (pairs), 1 thread")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-to-host (PCIe-inclusive) measurement")
     ap.add_argument("--workspace-gb", type=float, default=0.0,
-                    help="device budget (GB) for the 2-bit traceback codes; 0 = the library default (85%% of free HBM); batches above it run in chunks")
+                    help="device budget (GB) for the traceback codes; 0 = the library default (half the free "
+                         "HBM, <= 64 GiB) -- cfg3/4/5 default to 240; batches above it run in chunks")
     ap.add_argument("--no-parity", action="store_true")
+    ap.add_argument("--check-all", action="store_true",
+                    help="cfg5: check every pair's CIGAR path and score on the host (oracle cigar_check)")
     ap.add_argument("--gap-open", type=int, default=None,
                     help="affine-gap extension (no reference counterpart): a gap of length L costs "
                          "gap_open + L*gap, gap = the third --scoring value (config 5's 'affine gaps')")
-    ap.add_argument("--pipeline", action="store_true",
-                    help="run the K steps as one ta_plan_execute_batches call (batch k's traceback on a "
-                         "second stream beside batch k+1's fill) instead of ta_plan_execute per step; "
-                         "measured slower on config 2 (DESIGN.md 3.8)")
+    ap.add_argument("--flags", type=int, default=0, help="ta_plan_create TA_PLAN_* kernel-selection flags")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal only)")
-    a = ap.parse_args()
+    a = ap.parse_args(argv)
     if a.workload == "cfg2":
         a.pairs = a.pairs or 10000
         a.mode = a.mode or "local"
-    elif a.workload in ("cfg3", "cfg3map"):
+    elif a.workload in ("cfg3", "cfg4", "cfg3map"):
         a.pairs = a.pairs or 10000
         a.mode = a.mode or "semiGlobal"
         a.cpu_pairs = min(a.cpu_pairs, 200)
-    else:
+        a.cpu_pairs_1t = min(a.cpu_pairs_1t, 20)
+        a.workspace_gb = a.workspace_gb or 240.0
+    elif a.workload == "cfg5":
         # a slice of config 5's 100k pairs that fills the GPU in one chunk: 8,192 pairs (4,096
         # two-pair waves, 197 GB of 2-bit codes); affine 4,096 (4-bit codes, 197 GB)
         a.pairs = a.pairs or (8192 if a.gap_open is None else 4096)
@@ -103,14 +115,225 @@ def parse():
         a.qlen = a.tlen = 10000
         a.related = True
         a.cpu_pairs = min(a.cpu_pairs, 64 if a.gap_open is None else 32)
+        a.cpu_pairs_1t = min(a.cpu_pairs_1t, 4)
+        a.workspace_gb = a.workspace_gb or 240.0
     return a
 
 
-MODES = {"global": 0, "local": 1, "semiGlobal": 2}
+# --------------------------------------------------------------------------- ranks
 
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """--gpus N outside torch.distributed: start the N ranks as a child process
+    (nothing here has touched the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd, env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+
+
+class Dist:
+    """This process's rank, device and collective helpers (RCCL or gloo)."""
+
+    def __init__(self, args):
+        import torch
+
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.backend = args.dist_backend
+        self.dist = None
+        # TA_BENCH_ONE_GPU=1: every rank on device 0 (multi-rank rehearsal on a 1-GPU box, gloo)
+        self.dev_index = 0 if os.environ.get("TA_BENCH_ONE_GPU") == "1" else self.local_rank
+        torch.cuda.set_device(self.dev_index)
+        self.dev = torch.device("cuda", self.dev_index)
+        if self.world > 1:
+            import torch.distributed as dist
+
+            dist.init_process_group(self.backend, device_id=self.dev if self.backend == "nccl" else None)
+            self.dist = dist
+        # collectives run on device tensors with RCCL, on host tensors with gloo
+        self.cdev = self.dev if self.backend == "nccl" else torch.device("cpu")
+
+    def barrier(self):
+        if self.dist:
+            self.dist.barrier()
+
+    def max(self, x: float) -> float:
+        if not self.dist:
+            return x
+        import torch
+
+        t = torch.tensor([x], dtype=torch.float64, device=self.cdev)
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_gather_flat(self, out, t, async_op):
+        """out = concatenation over ranks of t (equal sizes)."""
+        if self.backend == "nccl":
+            return self.dist.all_gather_into_tensor(out, t, async_op=async_op)
+        parts = list(out.chunk(self.world))
+        return self.dist.all_gather(parts, t, async_op=async_op)
+
+    def close(self):
+        if self.dist:
+            self.dist.barrier()
+            self.dist.destroy_process_group()
+
+
+class ResultGather:
+    """Every step's results of every rank gathered to every rank (all_gather;
+    rank 0 is the consumer).  Records of step k: one all_gather right after its
+    kernels.  CIGAR bytes of step k (compacted on the device, ta_compact_cigars):
+    posted once step k+1 is enqueued -- their sizes ride in step k's records,
+    which by then have arrived without stalling the GPU -- padded to the largest
+    rank's byte count (RCCL has no gatherv)."""
+
+    def __init__(self, D: Dist, P_max: int, cigar: bool):
+        import torch
+
+        self.torch, self.D, self.P, self.cigar = torch, D, P_max, cigar
+        self.pending = []
+
+    def post(self, plan):
+        torch, D, P = self.torch, self.D, self.P
+        rec = torch.zeros(3 * P + 2, dtype=torch.int32, device=D.dev)
+        n = plan.P
+        rec[:n] = plan.score
+        rec[P:P + n] = plan.target_begin
+        dst = None
+        if self.cigar:
+            rec[2 * P:2 * P + n] = plan.cigar_len
+            dst, off = plan.compact_cigars()
+            rec[3 * P + 1] = off[-1].to(torch.int32)
+        rec[3 * P] = n
+        st = {"dst": dst}
+        if D.backend == "nccl":
+            out = torch.empty(D.world * rec.numel(), dtype=torch.int32, device=D.dev)
+            st["h"] = D.all_gather_flat(out, rec, True)
+            st["h"].wait()  # the current stream waits for the gather; the host does not
+            tot = torch.empty((D.world, 2), dtype=torch.int32, pin_memory=True)
+            tot.copy_(out.view(D.world, -1)[:, 3 * P:], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+            st.update(out=out, tot=tot, ev=ev)
+        else:
+            out = torch.empty(D.world * rec.numel(), dtype=torch.int32)
+            D.all_gather_flat(out, rec.cpu(), False)
+            st.update(out=out, tot=out.view(D.world, -1)[:, 3 * P:].clone(), ev=None)
+        if self.cigar and self.pending and "bytes" not in self.pending[-1]:
+            self._post_bytes(self.pending[-1])
+        self.pending.append(st)
+
+    def _post_bytes(self, st):
+        torch, D = self.torch, self.D
+        if st["ev"] is not None:
+            st["ev"].synchronize()  # step k's records are in: the GPU is already busy with step k+1
+        tot = st["tot"][:, 1].numpy()
+        words = max(1, (int(tot.max()) + 3) // 4)
+        dst = st["dst"]
+        if dst.numel() < 4 * words:
+            buf = torch.zeros(4 * words, dtype=torch.uint8, device=dst.device)
+            buf[:dst.numel()] = dst
+            dst = buf
+        mine = dst[:4 * words].view(torch.int32)
+        if D.backend == "nccl":
+            out = torch.empty(D.world * words, dtype=torch.int32, device=D.dev)
+            st["h2"] = D.all_gather_flat(out, mine, True)
+        else:
+            out = torch.empty(D.world * words, dtype=torch.int32)
+            D.all_gather_flat(out, mine.cpu(), False)
+            st["h2"] = None
+        st["bytes"] = (out, words)
+
+    def drain(self):
+        for st in self.pending:
+            if self.cigar and "bytes" not in st:
+                self._post_bytes(st)
+        for st in self.pending:
+            for h in (st.get("h"), st.get("h2")):
+                if h is not None:
+                    h.wait()
+
+    def last(self):
+        """Rank-ordered (scores, target_begins, cigar_lens, cigar bytes) of the last step."""
+        st = self.pending[-1]
+        P, W = self.P, self.D.world
+        rec = st["out"].view(W, -1).cpu().numpy()
+        n = rec[:, 3 * P]
+        sc = np.concatenate([rec[r, :n[r]] for r in range(W)])
+        tb = np.concatenate([rec[r, P:P + n[r]] for r in range(W)]).view(np.uint32)
+        cl = np.concatenate([rec[r, 2 * P:2 * P + n[r]] for r in range(W)]).view(np.uint32)
+        cig = None
+        if self.cigar:
+            out, words = st["bytes"]
+            by = out.view(W, words).cpu().numpy().view(np.uint8)
+            cig = b"".join(by[r, :rec[r, 3 * P + 1]].tobytes() for r in range(W))
+        return sc, tb, cl, cig
+
+    def clear_old(self, keep=2):
+        # finished steps (their byte gathers posted) can go; waits keep the allocator safe
+        while len(self.pending) > keep and "bytes" in self.pending[0]:
+            st = self.pending.pop(0)
+            for h in (st.get("h"), st.get("h2")):
+                if h is not None:
+                    h.wait()
+
+
+# --------------------------------------------------------------------------- inputs
+
+def make_batch(args, D, cells_split=None):
+    """This rank's batch (host PairBatch) and, for cfg5, its inputs in HBM."""
+    from bioinfo1_amd import shard, synth
+
+    P, rank, world = args.pairs, D.rank, D.world
+    if args.workload == "cfg3":
+        return synth.cfg3_batch(P, first_read=rank * P)[0], None, (rank * P, (rank + 1) * P)
+    if args.workload == "cfg4":
+        full = synth.cfg3_batch(P)[0]
+        cells = full.qlen.astype(np.int64) * full.tlen.astype(np.int64)
+        lo, hi = shard.range_split(cells, world)[rank]
+        return full.slice(lo, hi), full, (lo, hi)
+    if args.workload == "cfg5":
+        import torch
+
+        q, t = synth.related_batch_torch(P, args.qlen, args.tlen, 0x5EED, first_pair=rank * P, device=D.dev)
+        ql = np.full(P, args.qlen, np.uint32)
+        tl = np.full(P, args.tlen, np.uint32)
+        qoff = np.arange(P, dtype=np.uint64) * np.uint64(args.qlen)
+        toff = np.arange(P, dtype=np.uint64) * np.uint64(args.tlen)
+        shapes = synth.PairBatch(np.zeros(0, np.uint8), qoff, ql, np.zeros(0, np.uint8), toff, tl)
+        dev_in = (q, torch.from_numpy(qoff.view(np.int64)).to(D.dev), t,
+                  torch.from_numpy(toff.view(np.int64)).to(D.dev))
+        return shapes, dev_in, (rank * P, (rank + 1) * P)
+    gen = synth.related_batch if args.related else synth.uniform_batch
+    return gen(P, args.qlen, args.tlen, 0x5EED, first_pair=rank * P), None, (rank * P, (rank + 1) * P)
+
+
+def host_batch_of(batch, dev_in, k=None):
+    """A host PairBatch of (the first k pairs of) a batch whose bytes live in
+    HBM (cfg5: fixed shape, pairs back to back)."""
+    from bioinfo1_amd import synth
+
+    k = batch.n_pairs if k is None else min(k, batch.n_pairs)
+    if dev_in is None:
+        return batch if k == batch.n_pairs else batch.slice(0, k)
+    q, _, t, _ = dev_in
+    n, m = int(batch.qlen[0]), int(batch.tlen[0])
+    return synth.PairBatch(q[:k * n].cpu().numpy(), batch.qoff[:k].copy(), batch.qlen[:k].copy(),
+                           t[:k * m].cpu().numpy(), batch.toff[:k].copy(), batch.tlen[:k].copy())
+
+
+# --------------------------------------------------------------------------- checks and baselines
 
 def fill_alg_bytes(batch, cigar: bool, affine: bool = False) -> int:
-    """Algorithmic HBM bytes of one fill launch (DESIGN.md §5): the sequence
+    """Algorithmic HBM bytes of one fill launch (DESIGN.md §4): the sequence
     bytes read, the 2-bit (affine: 4-bit) traceback code per DP cell written
     (cigar on) and 16 B of per-pair results (score, target_begin, goal cell)."""
     n = batch.qlen.astype(np.int64)
@@ -121,25 +344,71 @@ def fill_alg_bytes(batch, cigar: bool, affine: bool = False) -> int:
     return int(b.sum())
 
 
-def cpu_baseline(batch, mode, sc, cigar, pairs, threads, gap_open=None):
+def cpu_threads() -> int:
+    """The host cores this process may use: OMP_NUM_THREADS when the box sets
+    it (the GPU box allots 16 CPUs per GPU), else the affinity mask."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    return int(env) if env and env.isdigit() else len(os.sched_getaffinity(0))
+
+
+def cpu_baseline(batch, mode, sc, cigar, pairs, pairs_1t, gap_open=None):
     from oracle.pyoracle import Oracle, Reference
 
     affine = gap_open is not None
     impl = Reference() if Reference.available() and not affine else Oracle()
-    sample = batch.slice(0, min(pairs, batch.n_pairs))
-    t0 = time.perf_counter()
-    if affine:  # the reference has no affine Align: the CPU definition (oracle/affine_oracle.c) is the baseline
-        res = impl.align_affine_batch(sample, mode, sc[0], sc[1], gap_open, sc[2], cigar, n_threads=threads)
-    else:
-        res = impl.align_batch(sample, mode, *sc, cigar, n_threads=threads)
-    dt = time.perf_counter() - t0
-    assert not res.status.any()
-    return {"value": round(sample.cells / dt / 1e9, 4), "unit": "GCUPS", "cores": threads, "kind": impl.kind,
-            "sample": f"first {sample.n_pairs} pairs of the same batch ({sample.cells:.3g} cells), "
-                      f"OpenMP over pairs, {dt:.2f} s wall",
+
+    def run(k, threads):
+        sample = batch.slice(0, min(k, batch.n_pairs))
+        t0 = time.perf_counter()
+        if affine:  # the reference has no affine Align: the CPU definition (oracle/affine_oracle.c) is the baseline
+            res = impl.align_affine_batch(sample, mode, sc[0], sc[1], gap_open, sc[2], cigar, n_threads=threads)
+        else:
+            res = impl.align_batch(sample, mode, *sc, cigar, n_threads=threads)
+        dt = time.perf_counter() - t0
+        assert not res.status.any()
+        return sample, dt
+
+    thr = cpu_threads()
+    sample, dt = run(pairs, thr)
+    s1, dt1 = run(pairs_1t, 1)
+    return {"value": round(sample.cells / dt / 1e9, 4), "unit": "GCUPS", "cores": thr, "kind": impl.kind,
+            "nproc": os.cpu_count(), "affinity_cpus": len(os.sched_getaffinity(0)),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"),
+            "sample": f"first {sample.n_pairs} pairs of the same batch ({sample.cells:.3g} cells), OpenMP over pairs "
+                      f"(schedule dynamic) on {thr} threads, {dt:.2f} s wall",
+            "value_1thread": round(s1.cells / dt1 / 1e9, 4),
+            "sample_1thread": f"first {s1.n_pairs} pairs ({s1.cells:.3g} cells), 1 thread, {dt1:.2f} s",
             "impl": "oracle/_ref/libref_align.so (reference team_alignment.cpp, g++ -O3)" if impl.kind == "reference"
             else ("oracle/liboracle.so (affine_oracle.c: the extension's CPU definition)" if affine
                   else "oracle/liboracle.so (C restatement)")}
+
+
+def digest_name(args, n_pairs):
+    if args.workload == "cfg2" and (args.mode, args.scoring, args.qlen, args.tlen) == ("local", "1,-1,-1", 1000, 1000) \
+            and n_pairs == 10000:
+        return ("cfg2_related_local" if args.related else "cfg2_local"), 10000
+    if args.workload in ("cfg3", "cfg4") and (args.mode, args.scoring) == ("semiGlobal", "1,-1,-1") and n_pairs >= 64:
+        return "cfg3_semi_sample", 64
+    if args.workload == "cfg5" and (args.mode, args.scoring) == ("semiGlobal", "1,-1,-1") and n_pairs >= 32:
+        return "cfg5_semi_sample", 32
+    return None, 0
+
+
+def parity_vs_digest(scores, tbs, clens, cigar_of, name, k):
+    """The first k pairs against the committed golden digest (made by the
+    reference) of the same seeded batch."""
+    with open(os.path.join(ROOT, "tests", "golden", f"digest_{name}.json")) as f:
+        meta = json.load(f)
+    d = np.load(os.path.join(ROOT, "tests", "golden", f"digest_{name}.npz"))
+    ok = bool(np.array_equal(scores[:k], d["scores"]) and np.array_equal(tbs[:k], d["target_begins"])
+              and np.array_equal(clens[:k], d["cigar_lens"]))
+    h = hashlib.sha256()
+    for p in range(k):
+        c = cigar_of(p)
+        h.update(len(c).to_bytes(4, "little"))
+        h.update(c)
+    ok = ok and h.hexdigest() == meta["cigar_sha256"]
+    return {"golden": f"tests/golden/digest_{name}", "pairs_checked": k, "bit_exact": ok}
 
 
 def parity_vs_oracle(res, batch, mode, sc, gap_open, k):
@@ -157,55 +426,353 @@ def parity_vs_oracle(res, batch, mode, sc, gap_open, k):
             "pairs_checked": sub.n_pairs, "bit_exact": ok}
 
 
-def parity_vs_digest(res, batch, args):
-    """Compare against the committed golden digest (made by the reference) of
-    this seeded batch, or of its first pairs (per-pair streams make the
-    digest batches prefixes of the bench batches)."""
-    name, k = None, batch.n_pairs
-    if args.workload == "cfg2" and (args.mode, args.scoring, args.qlen, args.tlen) == ("local", "1,-1,-1", 1000, 1000) \
-            and batch.n_pairs == 10000:
-        name = "cfg2_related_local" if args.related else "cfg2_local"
-    elif args.workload == "cfg3" and (args.mode, args.scoring) == ("semiGlobal", "1,-1,-1") and batch.n_pairs >= 64:
-        name, k = "cfg3_semi_sample", 64
-    elif args.workload == "cfg5" and (args.mode, args.scoring) == ("semiGlobal", "1,-1,-1") and batch.n_pairs >= 32:
-        name, k = "cfg5_semi_sample", 32
-    if name is None or res.cigar_lens is None or (args.gap_open or 0) != 0:
+def check_all(res, batch, mode, sc, gap_open):
+    """Every pair: the CIGAR is a valid path of the mode whose score is the
+    reported score (oracle cigar_check; size-independent), on host cores."""
+    from oracle.pyoracle import affine_cigar_check_batch, cigar_check_batch
+
+    t0 = time.perf_counter()
+    if gap_open is None:
+        st = cigar_check_batch(batch, mode, *sc, res.scores, res.target_begins, res.arena, res.cigar_offsets,
+                               res.cigar_lens)
+    else:
+        st = affine_cigar_check_batch(batch, mode, sc[0], sc[1], gap_open, sc[2], res.scores, res.target_begins,
+                                      res.arena, res.cigar_offsets, res.cigar_lens)
+    return {"pairs_checked": int(batch.n_pairs), "bad": int(np.count_nonzero(st)), "check_s": round(time.perf_counter() - t0, 2),
+            "checker": "oracle cigar_check (path validity + rescoring of every CIGAR)"}
+
+
+def dominant_kernel(plan, mode, cigar, affine):
+    m, c = MODES_INV[mode], str(cigar).lower()
+    if affine:
+        return f"affine_dual_fill_kernel<{m},{c}>" if plan.dual_pairs else f"affine_fill_kernel<{m},{c}>"
+    if plan.flex_pairs and plan.flex_pairs * 2 >= plan.P:
+        return f"flex_fill_kernel<{m},{c}>"
+    if plan.dual_pairs * 2 >= plan.P:
+        return f"dual_fill_kernel<{m},{c}>"
+    return f"fill_kernel<{m},{c},false>"
+
+
+MODES_INV = {0: "kGlobal", 1: "kLocal", 2: "kSemi"}
+
+
+def load_profile(name, tag):
+    p = os.path.join(ROOT, "profiles", name)
+    if not os.path.exists(p):
         return None
-    import hashlib
-
-    with open(os.path.join(ROOT, "tests", "golden", f"digest_{name}.json")) as f:
-        meta = json.load(f)
-    d = np.load(os.path.join(ROOT, "tests", "golden", f"digest_{name}.npz"))
-    ok = bool(np.array_equal(res.scores[:k], d["scores"]) and np.array_equal(res.target_begins[:k], d["target_begins"])
-              and np.array_equal(res.cigar_lens[:k], d["cigar_lens"]))
-    h = hashlib.sha256()
-    for p in range(k):
-        c = res.cigar(p)
-        h.update(len(c).to_bytes(4, "little"))
-        h.update(c)
-    ok = ok and h.hexdigest() == meta["cigar_sha256"]
-    return {"golden": f"tests/golden/digest_{name}", "pairs_checked": k, "bit_exact": ok}
+    with open(p) as f:
+        return json.load(f).get(tag)
 
 
-def workload_name(args, cigar):
+# --------------------------------------------------------------------------- workloads
+
+def main_align(args, D):
+    import torch
+
+    from bioinfo1_amd.align import Aligner, DevicePlan, HostBatchRunner
+
+    mode = MODES[args.mode]
+    sc = tuple(int(x) for x in args.scoring.split(","))
+    cigar = not args.no_cigar
+    affine = args.gap_open is not None
+    batch, aux, (lo, hi) = make_batch(args, D)
+    dev_in = aux if args.workload == "cfg5" else None
+    full = aux if args.workload == "cfg4" else None
+    al = Aligner(D.dev_index)
+    budget = int(args.workspace_gb * 2**30)
+    plan = DevicePlan(al, batch, mode, *sc, cigar, workspace_budget=budget, gap_open=args.gap_open,
+                      flags=args.flags, inputs=dev_in)
+    stream = torch.cuda.current_stream(D.dev)
+    P_max = plan.P
+    if args.workload == "cfg4" and D.world > 1:
+        from bioinfo1_amd import shard
+
+        cells = full.qlen.astype(np.int64) * full.tlen.astype(np.int64)
+        P_max = max(h - l for l, h in shard.range_split(cells, D.world))
+    gather = ResultGather(D, P_max, cigar) if D.world > 1 else None
+
+    def step():
+        plan.run()
+        if gather:
+            gather.post(plan)
+            gather.clear_old()
+
+    for _ in range(args.warmup):
+        step()
+    if gather:
+        gather.drain()
+    torch.cuda.synchronize(D.dev)
+    # parity of this rank's own results (rank 0: the digest covers the first pairs of the stream)
+    parity = None
+    if D.rank == 0 and not args.no_parity:
+        if args.warmup < 1:
+            plan.run()
+        res = plan.results()
+        name, k = digest_name(args, plan.P)
+        if name and cigar and not affine and lo == 0:
+            parity = parity_vs_digest(res.scores, res.target_begins, res.cigar_lens, res.cigar, name, k)
+        elif affine and cigar:
+            parity = parity_vs_oracle(res, host_batch_of(batch, dev_in, 16), mode, sc, args.gap_open, 16)
+    D.barrier()
+    torch.cuda.synchronize(D.dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    if gather:
+        gather.drain()
+    torch.cuda.synchronize(D.dev)
+    D.barrier()
+    torch.cuda.synchronize(D.dev)
+    elapsed = D.max(time.perf_counter() - t0)
+    plan.check()  # raises if a kernel reported an internal failure during the timed steps
+    ms = elapsed / max(args.steps, 1) * 1e3
+    cells_job = (full.cells if args.workload == "cfg4" else batch.cells * D.world)
+    gcups = cells_job / (ms / 1e3) / 1e9
+
+    gathered = None
+    if gather and D.rank == 0:
+        gathered = gather.last()
+
+    out = None
+    if D.rank == 0:
+        # dominant kernel (fill) timed on its own launch stream with HIP events
+        kt, tt = [], []
+        for _ in range(max(min(args.steps, 10), 3)):
+            f_ms = t_ms = 0.0
+            for c in range(plan.chunks):
+                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
+                e0.record(stream)
+                plan.run_fill(c)
+                e1.record(stream)
+                if cigar:
+                    plan.run_traceback(c)
+                e2.record(stream)
+                e2.synchronize()
+                f_ms += e0.elapsed_time(e1)
+                t_ms += e1.elapsed_time(e2)
+            kt.append(f_ms)
+            tt.append(t_ms)
+        fill_ms = float(np.mean(kt))
+        alg = fill_alg_bytes(batch, cigar, affine)
+        achieved = alg / (fill_ms / 1e3) / 1e9
+        tag = (f"{args.mode}_{'cigar' if cigar else 'score'}_{args.pairs}x{args.qlen}x{args.tlen}"
+               if args.workload not in ("cfg3", "cfg4") else f"cfg3_{'cigar' if cigar else 'score'}_{plan.P}")
+        if affine:
+            tag = "affine_" + tag
+        roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": load_profile("traffic.json", tag),
+                "traffic_source": "rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of this command, per fill launch "
+                                  "(profiles/traffic.json; scripts/profile.sh)",
+                "kernel": dominant_kernel(plan, mode, cigar, affine), "kernel_ms": round(fill_ms, 4),
+                "alg_bytes_per_launch": alg,
+                "note": "integer DP: VALU-bound, not HBM- or MFMA-bound (see valu)"}
+        ops = load_profile("valu.json", tag)
+        valu = {"kernel_gcups": round(batch.cells / (fill_ms / 1e3) / 1e9, 2),
+                "peak_int32_tops": round(VALU_PEAK_TOPS, 1), "valu_ops_per_cell": ops,
+                "frac": round(batch.cells * ops / (fill_ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 4) if ops else None}
+        extra = {}
+        if gathered is not None:
+            extra["gather"] = check_gathered(args, gathered, plan, full, al, mode, sc, cigar)
+        if D.world == 1 and not args.no_host and args.workload == "cfg2" and not affine:
+            extra["host_to_host"] = host_to_host(HostBatchRunner(al, batch, mode, *sc, cigar), batch, args)
+        if args.check_all and cigar:
+            extra["check_all"] = check_all(plan.results(), host_batch_of(batch, dev_in), mode, sc, args.gap_open)
+        cpu = None
+        if D.world == 1 and not args.no_cpu:
+            cpu = cpu_baseline(host_batch_of(batch, dev_in, args.cpu_pairs), mode, sc, cigar,
+                               args.cpu_pairs, args.cpu_pairs_1t, args.gap_open)
+        strong = args.workload == "cfg4"
+        out = {
+            "metric": METRIC, "value": round(gcups, 2), "unit": "GCUPS", "n_gpus": D.world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "strong" if strong else "weak", "vs_baseline": None, "dtype": DTYPE, "data": "synthetic",
+            "config": {"workload": workload_name(args, cigar, plan.P, full), "pairs_per_gpu": plan.P,
+                       "qlen": args.qlen if args.workload not in ("cfg3", "cfg4") else "1-20 kb reads",
+                       "tlen": args.tlen if args.workload not in ("cfg3", "cfg4") else "true-origin window",
+                       "mode": args.mode, "cigar": cigar, "cells_per_gpu": batch.cells, "cells_total": cells_job,
+                       "parallelism": (f"one read set range-split by cells over {D.world} GPU(s)" if strong else
+                                       f"pairs range-split over {D.world} GPU(s)")
+                       + (", RCCL all-gather of per-pair records and CIGAR bytes every step" if D.world > 1 else "")},
+            "fill_ms": round(fill_ms, 4), "traceback_ms": round(float(np.mean(tt)), 4) if cigar else None,
+            "batch_latency_ms": round(fill_ms + (float(np.mean(tt)) if cigar else 0.0), 4),
+            "chunks": plan.chunks, "workspace_gb": round(plan.workspace_bytes / 2**30, 2),
+            "plan": {"dual_pairs": plan.dual_pairs, "flex_pairs": plan.flex_pairs, "fused_traceback": plan.fused},
+            "roofline": roof, "valu": valu, "cpu_baseline": cpu, "parity": parity, **extra,
+            "device": torch.cuda.get_device_name(D.dev),
+        }
+    plan.close()
+    al.close()
+    D.close()
+    if out is not None:
+        print(json.dumps(out), flush=True)
+        if out.get("parity") and not out["parity"].get("bit_exact", True):
+            sys.exit(1)
+        g = out.get("gather")
+        if g and not g.get("bit_exact", True):
+            sys.exit(1)
+
+
+def check_gathered(args, gathered, plan, full, al, mode, sc, cigar):
+    """Rank 0 after the timed steps: the gathered results of all ranks.  cfg4:
+    byte-identical to the same read set aligned on this one GPU,
+    and its first 64 pairs to the reference digest.  cfg2: this rank's slice
+    of the gather equals its own results."""
+    sc_g, tb_g, cl_g, cig_g = gathered
+    if args.workload == "cfg4":
+        from bioinfo1_amd.align import DevicePlan
+
+        one = DevicePlan(al, full, mode, *sc, cigar, workspace_budget=int(args.workspace_gb * 2**30))
+        one.run()
+        r = one.results()
+        one.close()
+        ok = bool(np.array_equal(sc_g, r.scores) and np.array_equal(tb_g, r.target_begins))
+        if cigar:
+            ok = ok and np.array_equal(cl_g, r.cigar_lens) and cig_g == b"".join(r.cigars())
+        res = {"vs": "1-GPU result of the whole read set", "pairs": int(full.n_pairs), "bit_exact": ok,
+               "cigar_bytes": len(cig_g) if cig_g is not None else 0}
+        name, k = digest_name(args, full.n_pairs)
+        if name and cigar:
+            offs = np.concatenate([[0], np.cumsum(cl_g.astype(np.int64))])
+            d = parity_vs_digest(sc_g, tb_g, cl_g, lambda p: cig_g[offs[p]:offs[p + 1]], name, k)
+            res["digest"] = d
+            res["bit_exact"] = res["bit_exact"] and d["bit_exact"]
+        return res
+    r = plan.results()
+    n = plan.P
+    ok = bool(np.array_equal(sc_g[:n], r.scores) and np.array_equal(tb_g[:n], r.target_begins))
+    if cigar:
+        ok = ok and np.array_equal(cl_g[:n], r.cigar_lens) and cig_g[:int(r.cigar_lens.sum())] == b"".join(r.cigars())
+    return {"vs": "rank 0's own results (its slice of the gather)", "pairs_gathered": int(sc_g.shape[0]),
+            "bit_exact": ok, "cigar_bytes": len(cig_g) if cig_g is not None else 0}
+
+
+def host_to_host(runner, batch, args, reps=10):
+    """SURVEY §8d's GCUPS: inputs resident on the host (pinned) to results
+    (score, target_begin, CIGARs) on the host, one ta_align_batch per batch."""
+    runner.run()
+    runner.run()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        runner.run()
+    dt = (time.perf_counter() - t0) / reps
+    r = runner.results()
+    name, k = digest_name(args, batch.n_pairs)
+    par = parity_vs_digest(r.scores, r.target_begins, r.cigar_lens, r.cigar, name, k) if (name and r.cigar_lens is not None) else None
+    return {"value": round(batch.cells / dt / 1e9, 2), "unit": "GCUPS", "ms_per_batch": round(dt * 1e3, 4),
+            "batches": reps, "path": "ta_align_batch: pinned host SoA in -> H2D -> kernels -> D2H -> host results "
+                                     "(CIGARs compacted on the device)", "parity": par}
+
+
+def workload_name(args, cigar, n_pairs, full):
     tail = f"{args.mode}, scoring {args.scoring}, CIGAR {'on' if cigar else 'off'}"
     if args.workload == "cfg3":
         return (f"config 3 stand-in: {args.pairs} ONT-like reads per GPU (log-normal 1-20 kb, median 9 kb, 10% error, "
                 f"50% reverse) of a 4.64 Mb synthetic genome vs their true-origin windows, {tail}")
+    if args.workload == "cfg4":
+        return (f"config 4: one set of {full.n_pairs} ONT-like reads (config-3 stand-in) vs true-origin windows, "
+                f"range-split by cells over the GPUs, {tail}")
     pre = {"cfg2": "config 2: " if (args.qlen, args.tlen, args.pairs) == (1000, 1000, 10000) else "",
-           "cfg5": ("config 5 sample (linear gap): " if args.gap_open is None else
-                    f"config 5 sample, affine gaps (open {args.gap_open}, extend {args.scoring.split(',')[2]}): ")}[args.workload]
-    return pre + (f"{args.pairs} {'related' if args.related else 'uniform'} {args.qlen}x{args.tlen} pairs per GPU, "
+           "cfg5": (("config 5" if args.pairs >= 100000 else "config 5 slice") + " (linear gap): "
+                    if args.gap_open is None else
+                    ("config 5" if args.pairs >= 100000 else "config 5 slice")
+                    + f", affine gaps (open {args.gap_open}, extend {args.scoring.split(',')[2]}): ")}[args.workload]
+    return pre + (f"{n_pairs} {'related' if args.related else 'uniform'} {args.qlen}x{args.tlen} pairs per GPU, "
                   f"{tail}")
 
 
-def load_traffic(tag):
-    p = os.path.join(ROOT, "profiles", "traffic.json")
-    if not os.path.exists(p):
-        return None
-    with open(p) as f:
-        t = json.load(f)
-    return t.get(tag)
+def main_dropin(args):
+    """Single-call team::Align (the reference mapper's calling pattern) through
+    our drop-in library vs the reference's own Align, same harness, same pairs."""
+    res = {}
+    for name, exe in (("amd", os.path.join(ROOT, "build", "dropin_amd")),
+                      ("reference", os.path.join(ROOT, "oracle", "_ref", "dropin_ref"))):
+        if not os.path.exists(exe):
+            continue
+        rows = []
+        for thr in (1, 8):
+            p = subprocess.run([exe, str(thr), "1.0", "5x9,200x200,1000x1000", str(MODES[args.mode or "local"])],
+                               capture_output=True, text=True, timeout=300, check=True)
+            rows += [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
+        res[name] = rows
+    same = None
+    if "amd" in res and "reference" in res:
+        key = lambda r: (r["shape"], r["threads"])  # noqa: E731
+        ref = {key(r): r["score_checksum"] for r in res["reference"]}
+        same = all(ref.get(key(r)) == r["score_checksum"] for r in res["amd"])
+    print(json.dumps({"metric": "team::Align single-call throughput (drop-in, one pair per call)", "unit": "calls/s",
+                      "mode": args.mode or "local", "score_checksums_equal": same, "results": res}), flush=True)
+
+
+def main_mapper(args, D):
+    """config 3 end to end: the team_mapper pipeline on the GPU (minimizers ->
+    seed hits -> FindLIS -> one alignment batch) for this rank's reads against
+    the whole 4.64 Mb genome (index replicated per GPU, reads range-split)."""
+    import torch
+
+    from bioinfo1_amd import mapper as M
+    from bioinfo1_amd import shard, synth
+
+    mode = MODES[args.mode]
+    sc = tuple(int(x) for x in args.scoring.split(","))
+    g = synth.genome(synth.ECOLI_LEN)
+    rs = synth.ont_reads(args.pairs, g, first_read=D.rank * args.pairs)
+    reads = (rs.bytes if rs.bytes.size else np.zeros(1, np.uint8), rs.off.copy(), rs.len.copy())  # SoA, packed once
+    mp = M.Mapper(D.dev_index)
+    t0 = time.perf_counter()
+    idx = M.Index(mp, "ecoli_syn", g.tobytes(), 15, 5, 0.001)
+    index_s = time.perf_counter() - t0
+    opt = M.Options.make(type=mode, match=sc[0], mismatch=sc[1], gap=sc[2], want_cigar=not args.no_cigar,
+                         fastq_rules=True)
+
+    def step():
+        r = idx.map_batch(reads, opt)
+        if D.world > 1:  # gather every rank's records and CIGAR bytes in read order (RCCL over xGMI)
+            n_cig = int(r.cigar_len.sum()) if opt.want_cigar else 0
+            cig = torch.from_numpy(r.arena[:n_cig]).to(D.cdev) if opt.want_cigar else None
+            t = lambda a: torch.from_numpy(a.view(np.int32)).to(D.cdev)  # noqa: E731
+            shard.gather_results(D.dist, t(r.scores), t(r.t_begin), t(r.cigar_len), cig, device=D.cdev)
+        return r
+
+    for _ in range(args.warmup):
+        step()
+    D.barrier()
+    torch.cuda.synchronize(D.dev)
+    t0 = time.perf_counter()
+    stages = {}
+    for _ in range(args.steps):
+        r = step()
+        st, cells = mp.stage_times()
+        for k, v in st.items():
+            stages[k] = stages.get(k, 0.0) + v / args.steps
+    torch.cuda.synchronize(D.dev)
+    D.barrier()
+    elapsed = D.max(time.perf_counter() - t0)
+    ms = elapsed / max(args.steps, 1) * 1e3
+    out = None
+    if D.rank == 0:
+        extra = {}
+        if D.world == 1 and not args.no_cpu:
+            extra = mapper_cpu_baseline_and_parity(g, rs, 24, args.mode, os.path.join(ROOT, "gpurun_out", "cfg3map"))
+        out = {
+            "metric": METRIC, "value": round(cells * D.world / (ms / 1e3) / 1e9, 2), "unit": "GCUPS",
+            "n_gpus": D.world, "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3),
+            "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": DTYPE, "data": "synthetic",
+            "config": {"workload": f"config 3 end to end: {args.pairs} ONT-like reads per GPU (log-normal 1-20 kb, "
+                                   f"10% error, 50% reverse, FASTQ rules) mapped to a 4.64 Mb synthetic genome: GPU "
+                                   f"minimizers, seed matching, FindLIS, {args.mode} alignment of the chained windows "
+                                   f"with CIGAR {'off' if args.no_cigar else 'on'}; host reads in, host results out",
+                       "reads_per_gpu": args.pairs, "mode": args.mode, "aligned_cells_per_gpu": cells,
+                       "parallelism": f"reads range-split over {D.world} GPU(s), index replicated, RCCL all-gather "
+                                      f"of per-read records and CIGAR bytes"},
+            "reads_mapped": int(r.mapped.sum()), "reads_per_s": round(args.pairs * D.world / (ms / 1e3), 1),
+            "index_build_s": round(index_s, 3), "stage_ms": {k: round(v, 3) for k, v in stages.items()},
+            "roofline": None, "device": torch.cuda.get_device_name(D.dev), **extra,
+        }
+    idx.close()
+    mp.close()
+    D.close()
+    if out is not None:
+        print(json.dumps(out), flush=True)
 
 
 def write_fastx(path, recs, fastq):
@@ -221,8 +788,6 @@ def mapper_cpu_baseline_and_parity(genome, reads, sample, mode_name, tmpdir):
     """oracle/_ref/ref_mapper (the reference's Minimize + Align, restated glue,
     sequential) on the first `sample` reads, timed; and team_mapper_amd on the
     same files, whose PAF lines must be byte-identical."""
-    import subprocess
-
     from bioinfo1_amd import mapper as M
     from oracle.pymapper import REF_MAPPER_BIN
 
@@ -251,275 +816,20 @@ def mapper_cpu_baseline_and_parity(genome, reads, sample, mode_name, tmpdir):
     return res
 
 
-def main_mapper(args):
-    """config 3 end to end: the team_mapper pipeline on the GPU (minimizers ->
-    seed hits -> FindLIS -> one alignment batch) for this rank's reads against
-    the whole 4.64 Mb genome (index replicated per GPU, reads range-split)."""
-    from bioinfo1_amd import mapper as M
-
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group(args.dist_backend)
-    dev_index = 0 if os.environ.get("TA_BENCH_ONE_GPU") == "1" else local_rank
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
-    mode = MODES[args.mode]
-    sc = tuple(int(x) for x in args.scoring.split(","))
-    g = synth.genome(synth.ECOLI_LEN)
-    rs = synth.ont_reads(args.pairs, g, first_read=rank * args.pairs)
-    reads = (rs.bytes if rs.bytes.size else np.zeros(1, np.uint8), rs.off.copy(), rs.len.copy())  # SoA, packed once
-    mp = M.Mapper(dev_index)
-    t0 = time.perf_counter()
-    idx = M.Index(mp, "ecoli_syn", g.tobytes(), 15, 5, 0.001)
-    index_s = time.perf_counter() - t0
-    opt = M.Options.make(type=mode, match=sc[0], mismatch=sc[1], gap=sc[2], want_cigar=not args.no_cigar,
-                         fastq_rules=True)
-    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
-
-    def step():
-        r = idx.map_batch(reads, opt)
-        if world > 1:  # config 4: gather every rank's records and CIGAR bytes in read order (RCCL over xGMI)
-            from bioinfo1_amd import shard
-
-            n_cig = int(r.cigar_len.sum()) if opt.want_cigar else 0
-            cig = torch.from_numpy(r.arena[:n_cig]).to(coll_dev) if opt.want_cigar else None
-            t = lambda a: torch.from_numpy(a.view(np.int32)).to(coll_dev)  # noqa: E731
-            shard.gather_results(dist, t(r.scores), t(r.t_begin), t(r.cigar_len), cig, device=coll_dev)
-        return r
-
-    for _ in range(args.warmup):
-        step()
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    stages = {}
-    for _ in range(args.steps):
-        r = step()
-        st, cells = mp.stage_times()
-        for k, v in st.items():
-            stages[k] = stages.get(k, 0.0) + v / args.steps
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-    ms = elapsed / max(args.steps, 1) * 1e3
-    out = None
-    if rank == 0:
-        extra = {}
-        if world == 1 and not args.no_cpu:
-            extra = mapper_cpu_baseline_and_parity(g, rs, 24, args.mode, os.path.join(ROOT, "gpurun_out", "cfg3map"))
-        out = {
-            "metric": "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; bit-exact score+CIGAR",
-            "value": round(cells * world / (ms / 1e3) / 1e9, 2), "unit": "GCUPS", "n_gpus": world,
-            "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": f"config 3 end to end: {args.pairs} ONT-like reads per GPU (log-normal 1-20 kb, "
-                                   f"10% error, 50% reverse, FASTQ rules) mapped to a 4.64 Mb synthetic genome: GPU "
-                                   f"minimizers, seed matching, FindLIS, {args.mode} alignment of the chained windows "
-                                   f"with CIGAR {'off' if args.no_cigar else 'on'}; host reads in, host results out",
-                       "reads_per_gpu": args.pairs, "mode": args.mode, "aligned_cells_per_gpu": cells,
-                       "parallelism": f"reads range-split over {world} GPU(s), index replicated, RCCL all-gather "
-                                      f"of per-read records and CIGAR bytes (config 4 when world = 8)"},
-            "reads_mapped": int(r.mapped.sum()), "reads_per_s": round(args.pairs * world / (ms / 1e3), 1),
-            "index_build_s": round(index_s, 3), "stage_ms": {k: round(v, 3) for k, v in stages.items()},
-            "roofline": None, "device": torch.cuda.get_device_name(dev), **extra,
-        }
-    idx.close()
-    mp.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    if out is not None:
-        print(json.dumps(out), flush=True)
-
-
 def main():
     args = parse()
-    if args.workload == "cfg3map":
-        return main_mapper(args)
+    if args.workload == "dropin":
+        return main_dropin(args)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    dist = None
-    if world > 1:
-        import torch.distributed as dist
-
-        dist.init_process_group(args.dist_backend)
-    # TA_BENCH_ONE_GPU=1: every rank on device 0 (multi-rank rehearsal on a 1-GPU box, gloo)
-    dev_index = 0 if os.environ.get("TA_BENCH_ONE_GPU") == "1" else local_rank
-    torch.cuda.set_device(dev_index)
-    dev = torch.device("cuda", dev_index)
-    mode = MODES[args.mode]
-    sc = tuple(int(x) for x in args.scoring.split(","))
-    cigar = not args.no_cigar
-
-    # this rank's slice of the whole job: pairs [rank*P, (rank+1)*P) of the seeded stream
-    P = args.pairs
-    if args.workload == "cfg3":
-        batch = synth.cfg3_batch(P, first_read=rank * P)[0]
-    else:
-        gen = synth.related_batch if args.related else synth.uniform_batch
-        batch = gen(P, args.qlen, args.tlen, 0x5EED, first_pair=rank * P)
-
-    al = Aligner(dev_index)
-    plan = DevicePlan(al, batch, mode, *sc, cigar, workspace_budget=int(args.workspace_gb * 2**30),
-                      gap_open=args.gap_open)
-    stream = torch.cuda.current_stream(dev)
-    coll_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")  # gloo: host tensors
-    # Steps = batches.  --pipeline: ta_plan_execute_batches runs batch k's
-    # traceback beside batch k+1's fill; every batch has its own output
-    # buffers, so all K results stay intact and are gathered at the end.
-    pipelined = cigar and args.gap_open is None and args.pipeline
-    n_sets = max(args.steps, args.warmup, 2)
-    outs = [plan] + [plan.output_set() for _ in range(n_sets - 1)] if pipelined else None
-
-    def gather(sets):
-        if world > 1:  # range-split results -> every rank (RCCL all-gather over xGMI)
-            rec = torch.empty((len(sets), 3, P), dtype=torch.int32, device=dev)
-            for k, o in enumerate(sets):
-                rec[k, 0].copy_(o.score)
-                rec[k, 1].copy_(o.target_begin)
-                rec[k, 2].copy_(o.cigar_len if cigar else o.score)
-            rec = rec.to(coll_dev)
-            out = torch.empty((world * len(sets), 3, P), dtype=torch.int32, device=coll_dev)
-            # asynchronous: step k's gather overlaps step k+1's kernels; drained before the clock stops
-            pending.append((rec, out, dist.all_gather_into_tensor(out, rec, async_op=True)))
-
-    pending = []
-
-    def drain():
-        for _, _, h in pending:
-            h.wait()
-        pending.clear()
-
-    def run_steps(k):
-        if k <= 0:
-            return
-        if pipelined:
-            plan.run_batches(outs[:k])
-            gather(outs[:k])
-        else:
-            for _ in range(k):
-                plan.run()
-                gather([plan])
-
-    run_steps(args.warmup)
-    drain()
-    parity = None
-    if rank == 0 and not args.no_parity:
-        if args.warmup < (2 if pipelined else 1):
-            # compute only (rank 0 alone: no collective here)
-            plan.run_batches(outs[:2]) if pipelined else plan.run()
-        parity = parity_vs_digest(plan.results(), batch, args)
-        if parity is not None and pipelined:  # batch 1 ran beside batch 0 (capped traceback grid on its own)
-            p1 = parity_vs_digest(outs[1].results(), batch, args)
-            parity["pairs_checked"] += p1["pairs_checked"]
-            parity["bit_exact"] = parity["bit_exact"] and p1["bit_exact"]
-            parity["batches_checked"] = 2
-        if parity is None and args.gap_open is not None:
-            parity = parity_vs_oracle(plan.results(), batch, mode, sc, args.gap_open, 16)
-
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    run_steps(args.steps)
-    drain()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
-    ms = elapsed / max(args.steps, 1) * 1e3
-    cells_job = batch.cells * world
-    gcups = cells_job / (ms / 1e3) / 1e9
-
-    out = None
-    if rank == 0:
-        # dominant kernel (fill) timed on its own launch stream with HIP events
-        kt, tt = [], []
-        for _ in range(max(args.steps, 3)):
-            f_ms = t_ms = 0.0
-            for c in range(plan.chunks):
-                e0, e1, e2 = (torch.cuda.Event(enable_timing=True) for _ in range(3))
-                e0.record(stream)
-                plan.run_fill(c)
-                e1.record(stream)
-                if cigar:
-                    plan.run_traceback(c)
-                e2.record(stream)
-                e2.synchronize()
-                f_ms += e0.elapsed_time(e1)
-                t_ms += e1.elapsed_time(e2)
-            kt.append(f_ms)
-            tt.append(t_ms)
-        fill_ms = float(np.mean(kt))
-        alg = fill_alg_bytes(batch, cigar, args.gap_open is not None)
-        achieved = alg / (fill_ms / 1e3) / 1e9 if alg else None
-        tag = (f"{args.mode}_{'cigar' if cigar else 'score'}_{args.pairs}x{args.qlen}x{args.tlen}" if args.workload != "cfg3"
-               else f"cfg3_{'cigar' if cigar else 'score'}_{args.pairs}")
-        if args.gap_open is not None:
-            tag = "affine_" + tag
-        traffic = load_traffic(tag)
-        roof = {"bound": "hbm", "achieved": round(achieved, 2) if achieved else None, "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4) if achieved else None,
-                "traffic": traffic, "kernel": ("affine_dual_fill_kernel" if plan.dual_pairs else "affine_fill_kernel")
-                if args.gap_open is not None else "fill_kernel",
-                "kernel_ms": round(fill_ms, 4),
-                "alg_bytes_per_launch": alg,
-                "note": "integer DP: VALU-bound, not HBM- or MFMA-bound (see valu)"}
-        ops_per_cell = None
-        pv = os.path.join(ROOT, "profiles", "valu.json")
-        if os.path.exists(pv):
-            with open(pv) as f:
-                ops_per_cell = json.load(f).get(tag)
-        valu = {"kernel_gcups": round(batch.cells / (fill_ms / 1e3) / 1e9, 2), "peak_int32_tops": round(VALU_PEAK_TOPS, 1),
-                "valu_ops_per_cell": ops_per_cell,
-                "frac": round(batch.cells * ops_per_cell / (fill_ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 4)
-                if ops_per_cell else None}
-        cpu = None
-        if world == 1 and not args.no_cpu:
-            thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-            cpu = cpu_baseline(batch, mode, sc, cigar, args.cpu_pairs, thr, args.gap_open)
-        out = {
-            "metric": "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; bit-exact score+CIGAR",
-            "value": round(gcups, 2), "unit": "GCUPS", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True, "scaling": "weak",
-            "vs_baseline": None, "dtype": "int32", "data": "synthetic",
-            "config": {"workload": workload_name(args, cigar),
-                       "pairs_per_gpu": args.pairs, "qlen": args.qlen if args.workload != "cfg3" else "1-20 kb reads",
-                       "tlen": args.tlen if args.workload != "cfg3" else "true-origin window", "mode": args.mode,
-                       "cigar": cigar, "cells_per_gpu": batch.cells,
-                       "parallelism": f"pairs range-split over {world} GPU(s), RCCL all-gather of per-pair records"},
-            "fill_ms": round(fill_ms, 4), "traceback_ms": round(float(np.mean(tt)), 4) if cigar else None,
-            "pipelined": pipelined,
-            "batch_latency_ms": round(fill_ms + (float(np.mean(tt)) if cigar else 0.0), 4),
-            "chunks": plan.chunks, "workspace_gb": round(plan.workspace_bytes / 2**30, 2),
-            "roofline": roof, "valu": valu, "cpu_baseline": cpu, "parity": parity,
-            "device": torch.cuda.get_device_name(dev),
-        }
-    plan.close()
-    al.close()
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
-    if out is not None:
-        print(json.dumps(out), flush=True)
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr, flush=True)
+        sys.exit(3)
+    D = Dist(args)
+    if args.workload == "cfg3map":
+        return main_mapper(args, D)
+    return main_align(args, D)
 
 
 if __name__ == "__main__":

@@ -27,6 +27,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libteam_alignment.so")
 
 TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY, TA_ERR_RANGE = range(7)
+# ta_plan_create flags (include/team_align_c.h): kernel selection, same results
+TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED = 1, 2, 4
 
 
 class AlignmentType(enum.IntEnum):
@@ -71,8 +73,10 @@ def lib() -> C.CDLL:
     L.ta_cigar_slot_bytes.argtypes = [C.c_uint32, C.c_uint32]
     L.ta_align_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, u64p, u32p, C.c_void_p, u64p, u32p, C.c_int,
                                  C.c_int, C.c_int, C.c_int, C.c_int, i32p, u32p, C.c_void_p, C.c_uint64, u64p, u32p]
+    L.ta_context_release.argtypes = [C.c_void_p]
+    L.ta_context_release.restype = None
     L.ta_plan_create.argtypes = [C.c_void_p, C.c_uint32, u32p, u32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
-                                 C.c_uint64, C.POINTER(C.c_void_p)]
+                                 C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p)]
     L.ta_plan_destroy.argtypes = [C.c_void_p]
     L.ta_plan_destroy.restype = None
     for f in ("ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes"):
@@ -84,9 +88,11 @@ def lib() -> C.CDLL:
     L.ta_plan_dual_pairs.argtypes = [C.c_void_p]
     L.ta_plan_flex_pairs.restype = C.c_uint32
     L.ta_plan_flex_pairs.argtypes = [C.c_void_p]
+    L.ta_plan_fused.argtypes = [C.c_void_p]
     L.ta_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ta_plan_check.argtypes = [C.c_void_p]
-    L.ta_plan_execute_batches.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p]
+    L.ta_compact_cigars.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
+                                    C.c_void_p, C.c_void_p]
     L.ta_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     L.ta_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     # affine-gap extension (include/team_align_c.h, no reference counterpart)
@@ -94,7 +100,7 @@ def lib() -> C.CDLL:
                                         C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, i32p, u32p, C.c_void_p,
                                         C.c_uint64, u64p, u32p]
     L.ta_affine_plan_create.argtypes = [C.c_void_p, C.c_uint32, u32p, u32p, C.c_int, C.c_int, C.c_int, C.c_int,
-                                        C.c_int, C.c_int, C.c_uint64, C.POINTER(C.c_void_p)]
+                                        C.c_int, C.c_int, C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p)]
     L.ta_affine_plan_destroy.argtypes = [C.c_void_p]
     L.ta_affine_plan_destroy.restype = None
     for f in ("ta_affine_plan_cigar_slots_bytes", "ta_affine_plan_workspace_bytes"):
@@ -113,9 +119,10 @@ def lib() -> C.CDLL:
 
 # Every symbol include/team_align_c.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = [
-    "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_cigar_slot_bytes",
-    "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes", "ta_plan_workspace_bytes",
-    "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_execute", "ta_plan_execute_batches", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_execute_traceback",
+    "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_context_release",
+    "ta_cigar_slot_bytes", "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes",
+    "ta_plan_workspace_bytes", "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_fused",
+    "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_execute_traceback", "ta_compact_cigars",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
     "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
@@ -188,6 +195,10 @@ class Aligner:
     @property
     def handle(self):
         return self._h
+
+    def release(self):
+        """ta_context_release: free the cached device workspace and staging."""
+        lib().ta_context_release(self._h)
 
     def align_batch(self, batch, type, match: int, mismatch: int, gap: int, want_cigar: bool = True) -> BatchResult:
         """Batched team::Align over a bioinfo1_amd.synth.PairBatch."""
@@ -275,26 +286,6 @@ def _results(o) -> BatchResult:
     return BatchResult(sc, tb, start, ln, slots)
 
 
-class PlanOutputs:
-    """A second (third, ...) set of device outputs over a DevicePlan's inputs."""
-
-    def __init__(self, plan: "DevicePlan"):
-        torch = plan.torch
-        self.torch, self.dev, self.want_cigar, self.plan = torch, plan.dev, plan.want_cigar, plan
-        self.score = torch.zeros_like(plan.score)
-        self.target_begin = torch.zeros_like(plan.target_begin)
-        self.slots = torch.zeros_like(plan.slots)
-        self.cigar_start = torch.zeros_like(plan.cigar_start)
-        self.cigar_len = torch.zeros_like(plan.cigar_len)
-        self.io = _DeviceIO(plan.qbytes.data_ptr(), plan.qoff.data_ptr(), plan.tbytes.data_ptr(),
-                            plan.toff.data_ptr(), self.score.data_ptr(), self.target_begin.data_ptr(),
-                            self.slots.data_ptr(), self.cigar_start.data_ptr(), self.cigar_len.data_ptr())
-
-    def results(self) -> BatchResult:
-        self.plan.check()
-        return _results(self)
-
-
 class DevicePlan:
     """Device-resident batch: inputs and outputs are torch tensors in HBM.
 
@@ -303,9 +294,12 @@ class DevicePlan:
     current torch stream (asynchronous)."""
 
     def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, device=None,
-                 workspace_budget: int = 0, gap_open=None):
+                 workspace_budget: int = 0, gap_open=None, flags: int = 0, inputs=None):
         """gap_open=None: team::Align's linear gap.  gap_open=o: the affine-gap
-        extension (ta_affine_plan_*) with gap_extend = gap."""
+        extension (ta_affine_plan_*) with gap_extend = gap.  flags: TA_PLAN_*
+        kernel selection (tests / measurements; same results).  inputs: the
+        batch already in HBM as (query bytes, query offsets, target bytes,
+        target offsets) tensors -- then only batch.qlen / batch.tlen are read."""
         import torch
 
         L = lib()
@@ -321,16 +315,19 @@ class DevicePlan:
         scoring = (match, mismatch, gap_open, gap) if self.affine else (match, mismatch, gap)
         r = self._fn("ta_plan_create")(aligner.handle, self.P, _p(batch.qlen, C.c_uint32),
                                        _p(batch.tlen, C.c_uint32), t, *scoring, int(self.want_cigar),
-                                       workspace_budget, C.byref(h))
+                                       workspace_budget, flags, C.byref(h))
         if r != TA_OK:
             _raise(r, aligner.handle)
         self._h = h
         self._ctx = aligner.handle
-        f = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)  # noqa: E731
-        self.qbytes = f(batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8))
-        self.tbytes = f(batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8))
-        self.qoff = f(batch.qoff.view(np.int64))
-        self.toff = f(batch.toff.view(np.int64))
+        if inputs is None:
+            f = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(self.dev)  # noqa: E731
+            self.qbytes = f(batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8))
+            self.tbytes = f(batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8))
+            self.qoff = f(batch.qoff.view(np.int64))
+            self.toff = f(batch.toff.view(np.int64))
+        else:
+            self.qbytes, self.qoff, self.tbytes, self.toff = inputs
         self.score = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
         self.target_begin = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
         self.slots_bytes = int(self._fn("ta_plan_cigar_slots_bytes")(h))
@@ -345,6 +342,8 @@ class DevicePlan:
         self.chunks = int(self._fn("ta_plan_chunks")(h))
         self.dual_pairs = int(L.ta_affine_plan_dual_pairs(h)) if self.affine else int(L.ta_plan_dual_pairs(h))
         self.flex_pairs = 0 if self.affine else int(L.ta_plan_flex_pairs(h))
+        self.fused = False if self.affine else bool(L.ta_plan_fused(h))
+        self.aligner = aligner
 
     def _stream(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
@@ -364,20 +363,6 @@ class DevicePlan:
         if r != TA_OK:
             _raise(r, self._ctx)
 
-    def output_set(self) -> "PlanOutputs":
-        """Fresh device output buffers for the plan's inputs (one per batch of run_batches)."""
-        return PlanOutputs(self)
-
-    def run_batches(self, outs):
-        """ta_plan_execute_batches: one execution per PlanOutputs in ``outs``,
-        batch k's traceback beside batch k+1's fill (linear-gap plans)."""
-        if self.affine:
-            raise NotImplementedError("run_batches: linear-gap plans only")
-        arr = (_DeviceIO * len(outs))(*[o.io for o in outs])
-        r = lib().ta_plan_execute_batches(self._h, arr, len(outs), self._stream())
-        if r != TA_OK:
-            _raise(r, self._ctx)
-
     def check(self):
         """ta_plan_check after synchronising: raises DeviceError if a kernel reported an internal failure."""
         self.torch.cuda.synchronize(self.dev)
@@ -385,6 +370,22 @@ class DevicePlan:
             r = lib().ta_plan_check(self._h)
             if r != TA_OK:
                 _raise(r, self._ctx)
+
+    def compact_cigars(self):
+        """The CIGARs packed back to back on the device (ta_compact_cigars on
+        the current stream): returns (bytes uint8 tensor, int64 offsets
+        tensor [P+1]) -- what a rank hands to an RCCL gather."""
+        torch = self.torch
+        lens = self.cigar_len.to(torch.int64)
+        off = torch.zeros(self.P + 1, dtype=torch.int64, device=self.dev)
+        torch.cumsum(lens, 0, out=off[1:])
+        # a device-side bound keeps this free of host syncs: every CIGAR fits its slot
+        dst = torch.empty(max(self.slots_bytes, 1), dtype=torch.uint8, device=self.dev)
+        r = lib().ta_compact_cigars(self._ctx, self.P, self.slots.data_ptr(), self.cigar_start.data_ptr(),
+                                    self.cigar_len.data_ptr(), off.data_ptr(), dst.data_ptr(), self._stream())
+        if r != TA_OK:
+            _raise(r, self._ctx)
+        return dst, off
 
     def results(self) -> BatchResult:
         """Synchronise, check and copy results to host (CIGARs unpacked from slots)."""
@@ -401,3 +402,55 @@ class DevicePlan:
             self.close()
         except Exception:
             pass
+
+
+class HostBatchRunner:
+    """Repeated host-memory batches (ta_align_batch) over one batch whose
+    inputs and outputs live in pinned host memory (torch pin_memory, i.e.
+    hipHostMalloc): what a caller that keeps its reads in pinned buffers gets
+    host-to-host.  run() is one call: upload, kernels, download, sync."""
+
+    def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True):
+        import torch
+
+        self.t = _check_type(type)
+        self.sc = (match, mismatch, gap)
+        self.want_cigar = bool(want_cigar)
+        self.aligner = aligner
+        self.P = P = batch.n_pairs
+
+        def pinned(a):
+            a = np.ascontiguousarray(a)
+            t = torch.empty(max(a.nbytes, 1), dtype=torch.uint8, pin_memory=True)
+            v = t.numpy()[: a.nbytes].view(a.dtype)
+            v[...] = a.reshape(-1)
+            return t, v
+
+        self._keep = []
+        for name, a in (("qb", batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8)), ("qoff", batch.qoff),
+                        ("qlen", batch.qlen), ("tb", batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8)),
+                        ("toff", batch.toff), ("tlen", batch.tlen), ("score", np.zeros(P, np.int32)),
+                        ("tbeg", np.zeros(P, np.uint32)), ("coff", np.zeros(P, np.uint64)),
+                        ("clen", np.zeros(P, np.uint32))):
+            t, v = pinned(a)
+            self._keep.append(t)
+            setattr(self, name, v)
+        cap = int((2 * (batch.qlen.astype(np.uint64) + batch.tlen.astype(np.uint64)) + 2).sum()) if P else 1
+        t, self.arena = pinned(np.zeros(max(cap, 1), np.uint8))
+        self._keep.append(t)
+        self.cap = cap
+
+    def run(self):
+        L = lib()
+        r = L.ta_align_batch(
+            self.aligner.handle, self.P, self.qb.ctypes.data, _p(self.qoff, C.c_uint64), _p(self.qlen, C.c_uint32),
+            self.tb.ctypes.data, _p(self.toff, C.c_uint64), _p(self.tlen, C.c_uint32), self.t, *self.sc,
+            int(self.want_cigar), _p(self.score, C.c_int32), _p(self.tbeg, C.c_uint32), self.arena.ctypes.data,
+            self.cap, _p(self.coff, C.c_uint64), _p(self.clen, C.c_uint32))
+        if r != TA_OK:
+            _raise(r, self.aligner.handle)
+
+    def results(self) -> BatchResult:
+        if not self.want_cigar:
+            return BatchResult(self.score.copy(), self.tbeg.copy(), None, None, None)
+        return BatchResult(self.score.copy(), self.tbeg.copy(), self.coff.copy(), self.clen.copy(), self.arena.copy())

@@ -29,6 +29,7 @@
 // SALU with a 64-step tile of the lane stripe's codes held in two VGPRs, and
 // writes runs through the shared RunWriter (ta_device.h).
 #include <hip/hip_runtime.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <algorithm>
 #include <cstdlib>
@@ -40,6 +41,8 @@
 #include "../../include/team_align_c.h"
 #include "ta_context.h"
 #include "ta_device.h"
+#include "ta_host_batch.h"
+#include "ta_planner.h"
 #include "ta_packed.h"
 
 namespace ta {
@@ -787,24 +790,6 @@ hipError_t launch_affine_dual(int mode, bool cigar, const AffArgs& a, hipStream_
     return hipGetLastError();
 }
 
-// Every packed value of aff_dual_pass within int16, with margins: H from the
-// diagonal path below / any path above, E and F within one gap step of H, the
-// bias -ma*j, the -inf stand-ins (H - K) and one more step of candidates.
-bool affine_fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int open, int ext) {
-    if (mode == kLocal || n == 0 || m == 0) return false;
-    const long long N = n, M = m, mn = std::min(N, M), mx = std::max(N, M);
-    const long long lo_s = std::min({0LL, (long long)ma, (long long)mi});
-    const long long hi_s = std::max({0LL, (long long)ma, (long long)mi});
-    long long hlo = mn * lo_s;
-    if (mode == kGlobal) hlo += std::min(0LL, (long long)open) + mx * std::min(0LL, (long long)ext);
-    const long long hhi = mn * hi_s + (N + M) * (std::max(0LL, (long long)open) + std::max(0LL, (long long)ext));
-    const long long k = std::llabs(open) + std::llabs(ext) + 2;
-    const long long marg = 2 * k + 2 * std::llabs(ma) + std::llabs(mi) + 8;
-    const long long slo = hlo - std::max(0LL, (long long)ma) * M - marg;
-    const long long shi = hhi + std::max(0LL, -(long long)ma) * M + marg;
-    return slo >= -32000 && shi <= 32000;
-}
-
 hipError_t launch_affine_fill(int mode, bool cigar, const AffArgs& a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const dim3 g = aff_grid(a.count), b(kBlock);
@@ -839,23 +824,11 @@ hipError_t launch_affine_traceback(int mode, const AffArgs& a, hipStream_t s) {
 }  // namespace ta
 
 // ---------------------------------------------------------------------------
-// Host driver.
+// Host driver (the planning is ta_planner.cpp build_affine_plan).
 struct ta_affine_plan {
     ta_context* ctx = nullptr;
-    uint32_t n_pairs = 0;
-    int type = 0, match = 0, mismatch = 0, open = 0, extend = 0;
-    bool want_cigar = false;
-    std::vector<uint32_t> order;  // pairs by descending cells: the big ones start first
-    std::vector<uint32_t> singles, duals;  // int32 fill: pairs; packed fill: 2 pair ids per couple
-    std::vector<uint64_t> ptr_off, bnd_off, slot_off;
-    struct Chunk {
-        uint32_t begin, count;    // plan order (traceback)
-        uint32_t sbegin, scount;  // singles
-        uint32_t dbegin, dcount;  // couples
-        uint64_t ptr_entries, bnd_entries;
-    };
-    std::vector<Chunk> chunks;
-    uint64_t slots_bytes = 0, ws_ptr_entries = 0, ws_bnd_entries = 0;
+    ta::AffinePlan h;
+    void* own_block = nullptr;  // device arrays of a plan made by ta_affine_plan_create (one allocation)
     uint32_t *d_qlen = nullptr, *d_tlen = nullptr, *d_order = nullptr, *d_goal_i = nullptr, *d_goal_j = nullptr;
     uint32_t *d_singles = nullptr, *d_duals = nullptr;
     uint32_t* d_fb = nullptr;  // hand-back list [2 * couples], then one counter per chunk
@@ -864,203 +837,106 @@ struct ta_affine_plan {
 
 namespace {
 
-int afail(ta_context* ctx, int code, const std::string& msg) {
-    if (ctx) ctx->last_error = msg;
-    return code;
-}
+using ta_host::fail;
 
-#define TA_AHIP(ctx, expr)                                                                            \
-    do {                                                                                              \
-        hipError_t e_ = (expr);                                                                       \
-        if (e_ != hipSuccess)                                                                         \
-            return afail((ctx), TA_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(e_)); \
-    } while (0)
+struct AffOffs {
+    uint64_t qlen, tlen, order, singles, duals, ptr_off, bnd_off, slot_off;  // uploaded
+    uint64_t goal_i, goal_j, fb;                                             // device-only
+};
 
 template <class T>
-int aupload(ta_context* ctx, T** dptr, const std::vector<T>& v) {
-    if (v.empty()) return TA_OK;
-    TA_AHIP(ctx, hipMalloc(reinterpret_cast<void**>(dptr), v.size() * sizeof(T)));
-    TA_AHIP(ctx, hipMemcpy(*dptr, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
-    return TA_OK;
+uint64_t avbytes(const std::vector<T>& v) {
+    return v.size() * sizeof(T);
 }
 
-int agrow(ta_context* ctx, ta_context::Buf& b, size_t bytes) {
-    if (bytes <= b.cap) return TA_OK;
-    if (b.p) (void)hipFree(b.p);
-    b.p = nullptr;
-    b.cap = 0;
-    const size_t want = std::max<size_t>(bytes, 4096);
-    TA_AHIP(ctx, hipMalloc(&b.p, want));
-    b.cap = want;
-    return TA_OK;
+AffOffs aff_layout(const ta::AffinePlan& h, ta::BlockLayout& L) {
+    AffOffs o{};
+    o.qlen = L.add(avbytes(h.qlen));
+    o.tlen = L.add(avbytes(h.tlen));
+    o.order = L.add(avbytes(h.order));
+    o.singles = L.add(avbytes(h.singles));
+    o.duals = L.add(avbytes(h.duals));
+    o.ptr_off = L.add(avbytes(h.ptr_off));
+    o.bnd_off = L.add(avbytes(h.bnd_off));
+    o.slot_off = L.add(avbytes(h.slot_off));
+    return o;
 }
 
-uint64_t affine_default_budget(const ta_context* ctx) {
-    if (const char* e = std::getenv("TA_WORKSPACE_BYTES")) return std::strtoull(e, nullptr, 10);
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 48ull << 30;
-    const uint64_t avail = (uint64_t)free_b + ctx->ws_ptrs.cap + ctx->ws_bnd.cap;
-    return std::max<uint64_t>(avail / 100 * 85, 1ull << 30);
+void aff_layout_scratch(const ta::AffinePlan& h, ta::BlockLayout& L, AffOffs& o) {
+    o.goal_i = L.add(4ull * h.n_pairs);
+    o.goal_j = L.add(4ull * h.n_pairs);
+    o.fb = L.add(4ull * (h.duals.size() + h.chunks.size()));
 }
 
-}  // namespace
-
-extern "C" {
-
-void ta_affine_plan_destroy(ta_affine_plan* pl) {
-    if (!pl) return;
-    (void)hipSetDevice(pl->ctx->device);
-    for (void* p : {(void*)pl->d_qlen, (void*)pl->d_tlen, (void*)pl->d_order, (void*)pl->d_goal_i,
-                    (void*)pl->d_goal_j, (void*)pl->d_ptr_off, (void*)pl->d_bnd_off, (void*)pl->d_slot_off,
-                    (void*)pl->d_singles, (void*)pl->d_duals, (void*)pl->d_fb})
-        if (p) (void)hipFree(p);
-    delete pl;
+void aff_pack(const ta::AffinePlan& h, const AffOffs& o, uint8_t* base) {
+    auto put = [&](uint64_t at, const auto& v) {
+        if (!v.empty()) std::memcpy(base + at, v.data(), avbytes(v));
+    };
+    put(o.qlen, h.qlen);
+    put(o.tlen, h.tlen);
+    put(o.order, h.order);
+    put(o.singles, h.singles);
+    put(o.duals, h.duals);
+    put(o.ptr_off, h.ptr_off);
+    put(o.bnd_off, h.bnd_off);
+    put(o.slot_off, h.slot_off);
 }
 
-int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
-                          int match, int mismatch, int gap_open, int gap_extend, int want_cigar, uint64_t budget,
-                          ta_affine_plan** out) {
-    if (!ctx || !out || (n_pairs && (!qlen || !tlen))) return afail(ctx, TA_ERR_ARG, "null argument");
-    *out = nullptr;
-    if (type != TA_GLOBAL && type != TA_LOCAL && type != TA_SEMI_GLOBAL)
-        return afail(ctx, TA_ERR_BAD_TYPE, ta_status_string(TA_ERR_BAD_TYPE));
+void aff_bind(ta_affine_plan* pl, uint8_t* d, const AffOffs& o) {
+    auto u32 = [&](uint64_t at) { return reinterpret_cast<uint32_t*>(d + at); };
+    auto u64 = [&](uint64_t at) { return reinterpret_cast<uint64_t*>(d + at); };
+    pl->d_qlen = u32(o.qlen);
+    pl->d_tlen = u32(o.tlen);
+    pl->d_order = u32(o.order);
+    pl->d_singles = u32(o.singles);
+    pl->d_duals = u32(o.duals);
+    pl->d_ptr_off = u64(o.ptr_off);
+    pl->d_bnd_off = u64(o.bnd_off);
+    pl->d_slot_off = u64(o.slot_off);
+    pl->d_goal_i = u32(o.goal_i);
+    pl->d_goal_j = u32(o.goal_j);
+    pl->d_fb = u32(o.fb);
+}
+
+// the oracle's range (oracle_affine_in_range): every |value| < 2^26
+bool affine_in_range(uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int match, int mismatch,
+                     int gap_open, int gap_extend) {
     uint64_t maxn = 0, maxm = 0;
     for (uint32_t p = 0; p < n_pairs; ++p) {
         maxn = std::max<uint64_t>(maxn, qlen[p]);
         maxm = std::max<uint64_t>(maxm, tlen[p]);
     }
-    // the oracle's range (oracle_affine_in_range): every |value| < 2^26
     const long long pm = std::max({std::llabs(match), std::llabs(mismatch),
                                    std::llabs(gap_open) + std::llabs(gap_extend)});
-    if ((long long)(maxn + maxm + 2) * pm >= (1ll << 26))
-        return afail(ctx, TA_ERR_RANGE, ta_status_string(TA_ERR_RANGE));
-    TA_AHIP(ctx, hipSetDevice(ctx->device));
-    auto* pl = new ta_affine_plan();
-    pl->ctx = ctx;
-    pl->n_pairs = n_pairs;
-    pl->type = type;
-    pl->match = match;
-    pl->mismatch = mismatch;
-    pl->open = gap_open;
-    pl->extend = gap_extend;
-    pl->want_cigar = want_cigar != 0;
-    std::vector<uint32_t> byc(n_pairs);
-    std::iota(byc.begin(), byc.end(), 0u);
-    std::stable_sort(byc.begin(), byc.end(), [&](uint32_t x, uint32_t y) {
-        const uint64_t cx = (uint64_t)qlen[x] * tlen[x], cy = (uint64_t)qlen[y] * tlen[y];
-        if (cx != cy) return cx > cy;
-        return qlen[x] != qlen[y] ? qlen[x] > qlen[y] : tlen[x] > tlen[y];  // equal shapes adjacent
-    });
-    // units: couples of equal shape for the packed fill (global / semi, values
-    // within int16; TA_AFFINE_DUAL=0 disables), else single pairs
-    bool dual_ok = true;
-    if (const char* e = std::getenv("TA_AFFINE_DUAL")) dual_ok = std::atoi(e) != 0;
-    std::vector<std::pair<uint32_t, uint32_t>> units;  // (a, b); b == UINT32_MAX: single
-    for (uint32_t k = 0; k < n_pairs;) {
-        const uint32_t x = byc[k];
-        if (dual_ok && k + 1 < n_pairs && qlen[byc[k + 1]] == qlen[x] && tlen[byc[k + 1]] == tlen[x] &&
-            ta::affine_fits_int16(type, qlen[x], tlen[x], match, mismatch, gap_open, gap_extend)) {
-            units.push_back({x, byc[k + 1]});
-            k += 2;
-        } else {
-            units.push_back({x, UINT32_MAX});
-            ++k;
-        }
-    }
-    pl->slot_off.assign(n_pairs, 0);
-    uint64_t so = 0;
-    for (uint32_t p = 0; p < n_pairs; ++p) {
-        pl->slot_off[p] = so;
-        so += ta::cigar_slot_bytes(qlen[p], tlen[p]);
-    }
-    pl->slots_bytes = so;
-    if (!budget) budget = affine_default_budget(ctx);
-    const uint64_t budget_entries = std::max<uint64_t>(budget / sizeof(uint2), 1);
-    pl->ptr_off.assign(n_pairs, 0);
-    pl->bnd_off.assign(n_pairs, 0);
-    ta_affine_plan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0};
-    for (const auto& u : units) {
-        const uint32_t ids[2] = {u.first, u.second};
-        const int cnt = u.second == UINT32_MAX ? 1 : 2;
-        uint64_t pe = 0;
-        for (int h = 0; h < cnt; ++h) pe += pl->want_cigar ? ta::ptr_dwords(qlen[ids[h]], tlen[ids[h]]) : 0;
-        if (c.count && c.ptr_entries + pe > budget_entries) {
-            pl->chunks.push_back(c);
-            c = {(uint32_t)pl->order.size(), 0, (uint32_t)pl->singles.size(), 0, (uint32_t)(pl->duals.size() / 2), 0, 0, 0};
-        }
-        for (int h = 0; h < cnt; ++h) {
-            const uint32_t p = ids[h];
-            pl->ptr_off[p] = c.ptr_entries;
-            pl->bnd_off[p] = c.bnd_entries;
-            c.ptr_entries += pl->want_cigar ? ta::ptr_dwords(qlen[p], tlen[p]) : 0;
-            c.bnd_entries += ta::bnd_words(qlen[p], tlen[p]);
-            pl->order.push_back(p);
-            ++c.count;
-        }
-        if (cnt == 2) {
-            pl->duals.push_back(u.first);
-            pl->duals.push_back(u.second);
-            ++c.dcount;
-        } else {
-            pl->singles.push_back(u.first);
-            ++c.scount;
-        }
-    }
-    if (c.count) pl->chunks.push_back(c);
-    for (const auto& ch : pl->chunks) {
-        pl->ws_ptr_entries = std::max(pl->ws_ptr_entries, ch.ptr_entries);
-        pl->ws_bnd_entries = std::max(pl->ws_bnd_entries, ch.bnd_entries);
-    }
-    std::vector<uint32_t> ql(qlen, qlen + n_pairs), tl(tlen, tlen + n_pairs);
-    int rc = TA_OK;
-    auto up = [&](int r) {
-        if (rc == TA_OK) rc = r;
-    };
-    up(aupload(ctx, &pl->d_qlen, ql));
-    up(aupload(ctx, &pl->d_tlen, tl));
-    up(aupload(ctx, &pl->d_order, pl->order));
-    up(aupload(ctx, &pl->d_singles, pl->singles));
-    up(aupload(ctx, &pl->d_duals, pl->duals));
-    if (!pl->duals.empty()) up(aupload(ctx, &pl->d_fb, std::vector<uint32_t>(pl->duals.size() + pl->chunks.size(), 0u)));
-    up(aupload(ctx, &pl->d_ptr_off, pl->ptr_off));
-    up(aupload(ctx, &pl->d_bnd_off, pl->bnd_off));
-    up(aupload(ctx, &pl->d_slot_off, pl->slot_off));
-    if (rc == TA_OK && n_pairs) {
-        hipError_t e = hipMalloc(&pl->d_goal_i, n_pairs * 4ull);
-        if (e == hipSuccess) e = hipMalloc(&pl->d_goal_j, n_pairs * 4ull);
-        if (e != hipSuccess) rc = afail(ctx, TA_ERR_DEVICE, hipGetErrorString(e));
-    }
-    if (rc != TA_OK) {
-        ta_affine_plan_destroy(pl);
-        return rc;
-    }
-    *out = pl;
+    return (long long)(maxn + maxm + 2) * pm < (1ll << 26);
+}
+
+int affine_check_args(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
+                      int match, int mismatch, int gap_open, int gap_extend) {
+    if (!ctx) return TA_ERR_ARG;
+    if (n_pairs && (!qlen || !tlen)) return fail(ctx, TA_ERR_ARG, "null argument");
+    if (type != TA_GLOBAL && type != TA_LOCAL && type != TA_SEMI_GLOBAL)
+        return fail(ctx, TA_ERR_BAD_TYPE, ta_status_string(TA_ERR_BAD_TYPE));
+    if (!affine_in_range(n_pairs, qlen, tlen, match, mismatch, gap_open, gap_extend))
+        return fail(ctx, TA_ERR_RANGE, ta_status_string(TA_ERR_RANGE));
     return TA_OK;
 }
 
-uint64_t ta_affine_plan_cigar_slots_bytes(const ta_affine_plan* pl) { return pl ? pl->slots_bytes : 0; }
-uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* pl) {
-    return pl ? pl->ws_ptr_entries * sizeof(uint2) + pl->ws_bnd_entries * sizeof(int2) : 0;
-}
-uint32_t ta_affine_plan_chunks(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->chunks.size() : 0; }
-uint32_t ta_affine_plan_dual_pairs(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->duals.size() : 0; }
-
-static int affine_check_io(ta_affine_plan* pl, const ta_device_io* io) {
+int affine_check_io(ta_affine_plan* pl, const ta_device_io* io) {
     if (!pl || !io) return TA_ERR_ARG;
-    if (pl->n_pairs && (!io->query_off || !io->target_off || !io->score || !io->target_begin))
-        return afail(pl->ctx, TA_ERR_ARG, "null device pointer");
-    if (pl->want_cigar && pl->n_pairs && (!io->cigar_slots || !io->cigar_start || !io->cigar_len))
-        return afail(pl->ctx, TA_ERR_ARG, "null cigar device pointer");
+    if (pl->h.n_pairs && (!io->query_off || !io->target_off || !io->score || !io->target_begin))
+        return fail(pl->ctx, TA_ERR_ARG, "null device pointer");
+    if (pl->h.want_cigar && pl->h.n_pairs && (!io->cigar_slots || !io->cigar_start || !io->cigar_len))
+        return fail(pl->ctx, TA_ERR_ARG, "null cigar device pointer");
     return TA_OK;
 }
 
-static int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill,
-                             bool trace) {
+int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, bool fill, bool trace) {
     ta_context* ctx = pl->ctx;
-    TA_AHIP(ctx, hipSetDevice(ctx->device));
-    if (int r = agrow(ctx, ctx->ws_ptrs, pl->ws_ptr_entries * sizeof(uint2))) return r;
-    if (int r = agrow(ctx, ctx->ws_bnd, pl->ws_bnd_entries * sizeof(int2))) return r;
-    const auto& ch = pl->chunks[c];
+    const ta::AffinePlan& h = pl->h;
+    if (int r = ta_host::grow(ctx, ctx->ws_ptrs, h.ws_ptr_entries * sizeof(uint2))) return r;
+    if (int r = ta_host::grow(ctx, ctx->ws_bnd, h.ws_bnd_entries * sizeof(int2))) return r;
+    const auto& ch = h.chunks[c];
     ta::AffArgs a{};
     a.order = pl->d_order;
     a.begin = ch.begin;
@@ -1071,10 +947,10 @@ static int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStre
     a.tbytes = (const uint8_t*)io->target_bytes;
     a.toff = io->target_off;
     a.tlen = pl->d_tlen;
-    a.match = pl->match;
-    a.mismatch = pl->mismatch;
-    a.open = pl->open;
-    a.extend = pl->extend;
+    a.match = h.match;
+    a.mismatch = h.mismatch;
+    a.open = h.open;
+    a.extend = h.extend;
     a.ptrs = (uint2*)ctx->ws_ptrs.p;
     a.ptr_off = pl->d_ptr_off;
     a.bnd = (int2*)ctx->ws_bnd.p;
@@ -1088,51 +964,155 @@ static int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStre
     a.cigar_start = io->cigar_start;
     a.cigar_len = io->cigar_len;
     if (fill) {
+        roctxRangePushA("ta affine fill");
         if (ch.dcount) {  // packed couples, then the couples they hand back, on the same stream
             uint32_t* fb_list = pl->d_fb + 2ull * ch.dbegin;
-            uint32_t* fb_count = pl->d_fb + pl->duals.size() + c;
-            TA_AHIP(ctx, hipMemsetAsync(fb_count, 0, 4, s));
+            uint32_t* fb_count = pl->d_fb + h.duals.size() + c;
+            TA_HIP(ctx, hipMemsetAsync(fb_count, 0, 4, s));
             ta::AffArgs d = a;
             d.order = pl->d_duals;
             d.begin = ch.dbegin;
             d.count = ch.dcount;
             d.fb_list = fb_list;
             d.fb_count = fb_count;
-            TA_AHIP(ctx, ta::launch_affine_dual(pl->type, pl->want_cigar, d, s));
+            TA_HIP(ctx, ta::launch_affine_dual(h.type, h.want_cigar, d, s));
             ta::AffArgs f = a;
             f.order = fb_list;
             f.begin = 0;
             f.count = 2 * ch.dcount;
             f.count_dev = fb_count;
-            TA_AHIP(ctx, ta::launch_affine_fill(pl->type, pl->want_cigar, f, s));
+            TA_HIP(ctx, ta::launch_affine_fill(h.type, h.want_cigar, f, s));
         }
         ta::AffArgs sa = a;
         sa.order = pl->d_singles;
         sa.begin = ch.sbegin;
         sa.count = ch.scount;
-        TA_AHIP(ctx, ta::launch_affine_fill(pl->type, pl->want_cigar, sa, s));
+        TA_HIP(ctx, ta::launch_affine_fill(h.type, h.want_cigar, sa, s));
+        roctxRangePop();
     }
-    if (trace && pl->want_cigar) TA_AHIP(ctx, ta::launch_affine_traceback(pl->type, a, s));
+    if (trace && h.want_cigar) {
+        roctxRangePushA("ta affine traceback");
+        TA_HIP(ctx, ta::launch_affine_traceback(h.type, a, s));
+        roctxRangePop();
+    }
     return TA_OK;
 }
 
+int affine_exec(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t chunk, bool fill, bool trace) {
+    ta_context* ctx = pl->ctx;
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    if (int r = ta_host::stream_enter(ctx, s)) return r;
+    const uint32_t c0 = chunk == UINT32_MAX ? 0 : chunk;
+    const uint32_t c1 = chunk == UINT32_MAX ? (uint32_t)pl->h.chunks.size() : chunk + 1;
+    for (uint32_t c = c0; c < c1; ++c)
+        if (int r = affine_exec_chunk(pl, io, s, c, fill, trace)) return r;
+    return ta_host::stream_leave(ctx, s);
+}
+
+struct AffineHostPlan final : ta_host::HostPlan {
+    ta_affine_plan* pl;
+    AffOffs o{};
+    explicit AffineHostPlan(ta_affine_plan* p) : pl(p) {}
+    void layout(ta::BlockLayout& L) override { o = aff_layout(pl->h, L); }
+    void pack(uint8_t* base) override { aff_pack(pl->h, o, base); }
+    void layout_device_only(ta::BlockLayout& L) override { aff_layout_scratch(pl->h, L, o); }
+    void bind(uint8_t* dev) override { aff_bind(pl, dev, o); }
+    int execute(const ta_device_io* io, hipStream_t s) override {
+        return affine_exec(pl, io, s, UINT32_MAX, true, true);
+    }
+    uint64_t slots_bytes() const override { return pl->h.slots_bytes; }
+    uint64_t err_offset() const override { return UINT64_MAX; }
+    const char* err_message() const override { return ""; }
+};
+
+}  // namespace
+
+extern "C" {
+
+void ta_affine_plan_destroy(ta_affine_plan* pl) {
+    if (!pl) return;
+    if (pl->own_block) {
+        (void)hipSetDevice(pl->ctx->device);
+        (void)hipFree(pl->own_block);
+    }
+    delete pl;
+}
+
+int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
+                          int match, int mismatch, int gap_open, int gap_extend, int want_cigar, uint64_t budget,
+                          uint32_t flags, ta_affine_plan** out) {
+    if (!out) return TA_ERR_ARG;
+    *out = nullptr;
+    if (int r = affine_check_args(ctx, n_pairs, qlen, tlen, type, match, mismatch, gap_open, gap_extend)) return r;
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    auto* pl = new ta_affine_plan();
+    pl->ctx = ctx;
+    ta::build_affine_plan(pl->h, n_pairs, qlen, tlen, type, match, mismatch, gap_open, gap_extend, want_cigar != 0,
+                          budget ? budget : ta_host::default_budget(ctx), flags);
+    ta::BlockLayout L;
+    AffOffs o = aff_layout(pl->h, L);
+    const uint64_t upload = L.bytes;
+    aff_layout_scratch(pl->h, L, o);
+    std::vector<uint8_t> host(upload);
+    aff_pack(pl->h, o, host.data());
+    hipError_t e = hipMalloc(&pl->own_block, std::max<uint64_t>(L.bytes, 256));
+    if (e == hipSuccess) e = hipMemcpy(pl->own_block, host.data(), upload, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+        ta_affine_plan_destroy(pl);
+        return fail(ctx, TA_ERR_DEVICE, std::string("ta_affine_plan_create: ") + hipGetErrorString(e));
+    }
+    aff_bind(pl, static_cast<uint8_t*>(pl->own_block), o);
+    *out = pl;
+    return TA_OK;
+}
+
+uint64_t ta_affine_plan_cigar_slots_bytes(const ta_affine_plan* pl) { return pl ? pl->h.slots_bytes : 0; }
+uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* pl) {
+    return pl ? pl->h.ws_ptr_entries * sizeof(uint2) + pl->h.ws_bnd_entries * sizeof(int2) : 0;
+}
+uint32_t ta_affine_plan_chunks(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->h.chunks.size() : 0; }
+uint32_t ta_affine_plan_dual_pairs(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->h.duals.size() : 0; }
+
 int ta_affine_plan_execute(ta_affine_plan* pl, const ta_device_io* io, void* stream) {
     if (int r = affine_check_io(pl, io)) return r;
-    for (uint32_t c = 0; c < pl->chunks.size(); ++c)
-        if (int r = affine_exec_chunk(pl, io, (hipStream_t)stream, c, true, true)) return r;
-    return TA_OK;
+    std::lock_guard<std::mutex> lock(pl->ctx->mu);
+    return affine_exec(pl, io, (hipStream_t)stream, UINT32_MAX, true, true);
 }
 
 int ta_affine_plan_execute_fill(ta_affine_plan* pl, const ta_device_io* io, void* stream, uint32_t chunk) {
     if (int r = affine_check_io(pl, io)) return r;
-    if (chunk >= pl->chunks.size()) return pl->n_pairs ? TA_ERR_ARG : TA_OK;
-    return affine_exec_chunk(pl, io, (hipStream_t)stream, chunk, true, false);
+    if (chunk >= pl->h.chunks.size()) return pl->h.n_pairs ? TA_ERR_ARG : TA_OK;
+    std::lock_guard<std::mutex> lock(pl->ctx->mu);
+    return affine_exec(pl, io, (hipStream_t)stream, chunk, true, false);
 }
 
 int ta_affine_plan_execute_traceback(ta_affine_plan* pl, const ta_device_io* io, void* stream, uint32_t chunk) {
     if (int r = affine_check_io(pl, io)) return r;
-    if (chunk >= pl->chunks.size()) return pl->n_pairs ? TA_ERR_ARG : TA_OK;
-    return affine_exec_chunk(pl, io, (hipStream_t)stream, chunk, false, true);
+    if (chunk >= pl->h.chunks.size()) return pl->h.n_pairs ? TA_ERR_ARG : TA_OK;
+    std::lock_guard<std::mutex> lock(pl->ctx->mu);
+    return affine_exec(pl, io, (hipStream_t)stream, chunk, false, true);
+}
+
+int ta_align_batch_affine(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff,
+                          const uint32_t* qlen, const char* tbytes, const uint64_t* toff, const uint32_t* tlen,
+                          int type, int match, int mismatch, int gap_open, int gap_extend, int want_cigar,
+                          int32_t* score, uint32_t* target_begin, char* arena, uint64_t arena_bytes,
+                          uint64_t* cigar_off, uint32_t* cigar_len) {
+    uint64_t qend = 0, tend = 0;
+    if (int r = ta_host::check_host_batch(ctx, type, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, want_cigar, arena,
+                                          cigar_off, cigar_len, &qend, &tend))
+        return r;
+    if (n_pairs == 0) return TA_OK;
+    if (int r = affine_check_args(ctx, n_pairs, qlen, tlen, type, match, mismatch, gap_open, gap_extend)) return r;
+    std::lock_guard<std::mutex> lock(ctx->mu);
+    TA_HIP(ctx, hipSetDevice(ctx->device));
+    ta_affine_plan pl;
+    pl.ctx = ctx;
+    ta::build_affine_plan(pl.h, n_pairs, qlen, tlen, type, match, mismatch, gap_open, gap_extend, want_cigar != 0,
+                          ta_host::batch_budget(ctx, n_pairs, qlen, tlen, want_cigar, sizeof(uint2)), 0);
+    AffineHostPlan hp(&pl);
+    return ta_host::host_batch(ctx, hp, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, qend, tend, want_cigar, score,
+                               target_begin, arena, arena_bytes, cigar_off, cigar_len);
 }
 
 }  // extern "C"

@@ -6,41 +6,18 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "ta_layout.h"
+
 namespace ta {
-
-// Geometry of the fill: one wave64 per pair; lane l owns kRows consecutive
-// query rows; a "pass" is the 64*kRows = 1024 rows one wave covers at once.
-constexpr int kRows = 16;
-constexpr int kWave = 64;
-constexpr int kPassRows = kRows * kWave;
-constexpr int kWavesPerBlock = 4;
-constexpr int kBlock = kWave * kWavesPerBlock;
-
-enum Mode : int { kGlobal = 0, kLocal = 1, kSemi = 2 };
 
 // 2-bit traceback code per cell, code = (D bit << 1) | I bit.  One dword per
 // (pass, step, lane) holds the 16 rows of the lane's stripe as two bit
 // planes: D plane in bits 31:16 (row r at bit 31 - r), I plane in bits 15:0
-// (row r at bit 15 - r).  Local mode stores canonical codes (M=00 I=01 D=10
-// STOP=11); global / semi-global store the raw compares (up > max(diag,left),
-// left > diag), so there D wins whenever its bit is set (10 and 11 are D).
+// (row r at bit 15 - r).  The int32 local fill stores canonical codes (M=00
+// I=01 D=10 STOP=11); the other fills store the raw compares (up >
+// max(diag,left), left > diag), so D wins whenever its bit is set.
 enum Code : uint32_t { kCodeM = 0, kCodeI = 1, kCodeD = 2, kCodeStop = 3 };
 constexpr int kDPlane = 16;  // bit offset of the D plane
-
-// Steps of one pass over an m-column target: m + 63 (lane skew).
-__host__ __device__ inline uint32_t pass_steps(uint32_t m) { return m + kWave - 1; }
-__host__ __device__ inline uint32_t n_passes(uint32_t n) { return (n + kPassRows - 1) / kPassRows; }
-// Pointer-matrix dwords for an n x m pair: passes x steps x 64 lanes.
-__host__ __device__ inline uint64_t ptr_dwords(uint32_t n, uint32_t m) {
-    return (n == 0 || m == 0) ? 0 : (uint64_t)n_passes(n) * pass_steps(m) * kWave;
-}
-// Pass-boundary row (int32 per column) needed only when the query spans > 1 pass.
-__host__ __device__ inline uint64_t bnd_words(uint32_t n, uint32_t m) {
-    return n_passes(n) > 1 ? (uint64_t)m + 1 + kWave : 0;
-}
-__host__ __device__ inline uint64_t cigar_slot_bytes(uint32_t n, uint32_t m) {
-    return 2ull * ((uint64_t)n + m) + 2;
-}
 
 struct FillArgs {
     const uint32_t* order;  // visit order (pair ids); kernel handles order[begin .. begin+count)
@@ -118,22 +95,17 @@ struct CompactArgs {
 hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_fill_mode(bool wide, const FillArgs& a, hipStream_t s);
-// max_waves > 0 caps the grid (the kernel strides over the pairs)
-hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, uint32_t max_waves = 0);
+hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s);
 // Dual-pair packed int16 fill (ta_dual.hip): a.order holds 2 pair ids per wave.
 hipError_t launch_dual(int mode, bool cigar, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_dual_mode(const FillArgs& a, hipStream_t s);
-// Can an n x m pair run in the packed int16 kernel without overflow?
-bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
 // Flexible two-pair fill (ta_flex.hip, global / semi-global): a.order holds 2
 // pair ids per wave, the larger n first; both with the same pass count and
 // n mod 16; rebased int16 values, so any length fits.
 hipError_t launch_flex(int mode, bool cigar, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_flex_mode(const FillArgs& a, hipStream_t s);
-// Scoring whose rebased 16-bit values cannot overflow in the flexible fill.
-bool flex_fits(int mode, int match, int mismatch, int gap);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
 
 }  // namespace ta

@@ -389,10 +389,7 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
 #ifdef TA_TU_MISC
 template <int MODE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void traceback_kernel(TraceArgs a) {
-    // Wave-strided over the pairs: one wave per pair when the grid covers
-    // them all, fewer resident waves (each walking several pairs) when the
-    // launch is capped so it fits beside the next batch's fill (see
-    // ta_plan_execute_batches).
+    // Wave-strided over the pairs (one wave per pair: the grid covers them all).
     const int lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * kWavesPerBlock;
     for (uint32_t widx = wave_id(); widx < a.count; widx += stride) {
@@ -480,39 +477,9 @@ hipError_t launch_flex(int mode, bool cigar, const FillArgs& a, hipStream_t s) {
     }
 }
 
-// The flexible fill keeps V = S - O within a wave's span: 1,024 rows + 2 x 64
-// columns of cells whose neighbours differ by at most |score| + |gap| <= 2*mag
-// (plus the 64-step drift between rebases).
-bool flex_fits(int mode, int ma, int mi, int gap) {
-    if (mode == kLocal) return false;
-    const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
-    return (kPassRows + 3LL * kWave) * 2 * mag * 2 <= 30000;
-}
-
-// Bounds of the biased 16-bit values of ta_dual.hip (S and every candidate),
-// with a margin; pairs that do not fit run in the int32 kernel.
-bool fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {
-    if (n == 0 || m == 0) return false;
-    const long long N = n, M = m;
-    const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
-    const long long hmax = std::min(N, M) * std::max({0LL, (long long)ma, (long long)mi}) + (N + M) * std::max(0LL, (long long)gap);
-    long long lo, hi;
-    if (mode == kLocal) {
-        const long long z = 1 - 16LL * ma;  // S = 16H + z*j - i
-        hi = 16 * hmax + std::max(0LL, z) * M + 32 * mag;
-        lo = std::min(0LL, z) * M - N - 32 * mag;
-        if (16 * hmax + 15 > 32767) return false;  // the argmax key 16H + 15 - r
-    } else {  // S = H - ma*j
-        const long long hmin = -(N + M) * mag;
-        hi = hmax + std::max(0LL, -(long long)ma) * M + 4 * mag;
-        lo = hmin - std::max(0LL, (long long)ma) * M - 4 * mag;
-    }
-    return hi <= 32000 && lo >= -32000;
-}
-
-hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, uint32_t max_waves) {
+hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s) {
     if (!a.count) return hipSuccess;
-    const dim3 g = grid_for(max_waves ? std::min(a.count, max_waves) : a.count), b(kBlock);
+    const dim3 g = grid_for(a.count), b(kBlock);
     switch (mode) {
         case kGlobal: hipLaunchKernelGGL(traceback_kernel<kGlobal>, g, b, 0, s, a); break;
         case kLocal: hipLaunchKernelGGL(traceback_kernel<kLocal>, g, b, 0, s, a); break;

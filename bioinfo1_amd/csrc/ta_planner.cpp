@@ -1,0 +1,319 @@
+// bioinfo1_amd/csrc/ta_planner.cpp -- host planning of linear-gap and affine
+// batches (ta_planner.h).  No HIP: the device drivers (ta_api.hip,
+// ta_affine.hip) upload what this computes.
+#include "ta_planner.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <numeric>
+
+namespace ta {
+
+// The flexible fill keeps V = S - O within a wave's span: 1,024 rows + 2 x 64
+// columns of cells whose neighbours differ by at most |score| + |gap| <= 2*mag
+// (plus the 64-step drift between rebases).
+bool flex_fits(int mode, int ma, int mi, int gap) {
+    if (mode == kLocal) return false;
+    const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
+    return (kPassRows + 3LL * kWave) * 2 * mag * 2 <= 30000;
+}
+
+// Bounds of the biased 16-bit values of ta_dual.hip (S and every candidate),
+// with a margin; pairs that do not fit run in the int32 kernel.
+bool fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {
+    if (n == 0 || m == 0) return false;
+    const long long N = n, M = m;
+    const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
+    const long long hmax = std::min(N, M) * std::max({0LL, (long long)ma, (long long)mi}) + (N + M) * std::max(0LL, (long long)gap);
+    long long lo, hi;
+    if (mode == kLocal) {
+        const long long z = 1 - 16LL * ma;  // S = 16H + z*j - i
+        hi = 16 * hmax + std::max(0LL, z) * M + 32 * mag;
+        lo = std::min(0LL, z) * M - N - 32 * mag;
+        if (16 * hmax + 15 > 32767) return false;  // the argmax key 16H + 15 - r
+    } else {  // S = H - ma*j
+        const long long hmin = -(N + M) * mag;
+        hi = hmax + std::max(0LL, -(long long)ma) * M + 4 * mag;
+        lo = hmin - std::max(0LL, (long long)ma) * M - 4 * mag;
+    }
+    return hi <= 32000 && lo >= -32000;
+}
+
+// Every packed value of aff_dual_pass within int16, with margins: H from the
+// diagonal path below / any path above, E and F within one gap step of H, the
+// bias -ma*j, the -inf stand-ins (H - K) and one more step of candidates.
+bool affine_fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int open, int ext) {
+    if (mode == kLocal || n == 0 || m == 0) return false;
+    const long long N = n, M = m, mn = std::min(N, M), mx = std::max(N, M);
+    const long long lo_s = std::min({0LL, (long long)ma, (long long)mi});
+    const long long hi_s = std::max({0LL, (long long)ma, (long long)mi});
+    long long hlo = mn * lo_s;
+    if (mode == kGlobal) hlo += std::min(0LL, (long long)open) + mx * std::min(0LL, (long long)ext);
+    const long long hhi = mn * hi_s + (N + M) * (std::max(0LL, (long long)open) + std::max(0LL, (long long)ext));
+    const long long k = std::llabs(open) + std::llabs(ext) + 2;
+    const long long marg = 2 * k + 2 * std::llabs(ma) + std::llabs(mi) + 8;
+    const long long slo = hlo - std::max(0LL, (long long)ma) * M - marg;
+    const long long shi = hhi + std::max(0LL, -(long long)ma) * M + marg;
+    return slo >= -32000 && shi <= 32000;
+}
+
+namespace {
+
+// Pairs by descending cells (fewer stragglers: the big ones start first),
+// equal shapes adjacent so they can be coupled for the two-pair kernels.
+std::vector<uint32_t> by_cells(uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen) {
+    std::vector<uint32_t> o(n_pairs);
+    std::iota(o.begin(), o.end(), 0u);
+    bool uniform = true;
+    for (uint32_t p = 1; p < n_pairs && uniform; ++p) uniform = qlen[p] == qlen[0] && tlen[p] == tlen[0];
+    if (uniform) return o;  // already in order (stable)
+    std::stable_sort(o.begin(), o.end(), [&](uint32_t a, uint32_t b) {
+        const uint64_t ca = (uint64_t)qlen[a] * tlen[a], cb = (uint64_t)qlen[b] * tlen[b];
+        if (ca != cb) return ca > cb;
+        return qlen[a] != qlen[b] ? qlen[a] > qlen[b] : tlen[a] > tlen[b];
+    });
+    return o;
+}
+
+std::vector<uint64_t> slot_offsets(uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, uint64_t* total) {
+    std::vector<uint64_t> off(n_pairs);
+    uint64_t so = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        off[p] = so;
+        so += cigar_slot_bytes(qlen[p], tlen[p]);
+    }
+    *total = so;
+    return off;
+}
+
+}  // namespace
+
+void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type, int match,
+                int mismatch, int gap, bool want_cigar, uint64_t budget, uint32_t flags) {
+    pl = Plan{};
+    pl.n_pairs = n_pairs;
+    pl.type = type;
+    pl.match = match;
+    pl.mismatch = mismatch;
+    pl.gap = gap;
+    pl.want_cigar = want_cigar;
+    pl.qlen.assign(qlen, qlen + n_pairs);
+    pl.tlen.assign(tlen, tlen + n_pairs);
+    // Local mode keeps V = 32*score + row tag in int32; take the unscaled
+    // ("wide") kernel when any local value could reach 2^25 in magnitude.
+    uint64_t maxlen = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) maxlen = std::max<uint64_t>(maxlen, (uint64_t)qlen[p] + tlen[p]);
+    const uint64_t mag = std::max<uint64_t>({1ull, (uint64_t)std::llabs(match), (uint64_t)std::llabs(mismatch),
+                                             (uint64_t)std::llabs(gap)});
+    pl.wide = (type == kLocal) && (maxlen * mag >= (1ull << 25));
+    const bool dual = !(flags & kPlanInt32Only);
+    const std::vector<uint32_t> order = by_cells(n_pairs, qlen, tlen);
+    pl.slot_off = slot_offsets(n_pairs, qlen, tlen, &pl.slots_bytes);
+    const uint64_t budget_dw = std::max<uint64_t>(budget / 4, 1);
+    pl.ptr_off.assign(n_pairs, 0);
+    pl.bnd_off.assign(n_pairs, 0);
+    // Work units: one pair (int32 fill), an equal-shape couple (dual fill) or
+    // a couple of different shapes (flexible dual fill), then longest first.
+    struct Unit {
+        int kind;  // 0 single, 1 dual, 2 flex
+        uint32_t a, b;
+        uint64_t cost;  // cells one wave sweeps
+    };
+    std::vector<Unit> units;
+    units.reserve(n_pairs);
+    std::vector<uint32_t> rest;
+    const bool flex_ok = dual && !(flags & kPlanNoFlex) && flex_fits(type, match, mismatch, gap);
+    for (uint32_t k = 0; k < n_pairs;) {
+        const uint32_t p = order[k];
+        const uint32_t n = qlen[p], m = tlen[p];
+        // (equal shapes within int16 stay on the dual fill even when multi-pass: measured faster
+        // than the pipelined flexible fill on config 5, 4,056 vs 3,765 GCUPS)
+        const bool couple = dual && k + 1 < n_pairs && qlen[order[k + 1]] == n && tlen[order[k + 1]] == m &&
+                            fits_int16(type, n, m, match, mismatch, gap);
+        if (couple) {
+            units.push_back({1, p, order[k + 1], (uint64_t)n * m});
+            k += 2;
+        } else {
+            rest.push_back(p);
+            ++k;
+        }
+    }
+    if (flex_ok) {
+        // flexible couples: same pass count and n mod 16 (same rows in the last
+        // lane), neighbours by (n, m), at most 25 % of the wave's cells wasted
+        std::vector<uint32_t> cand;
+        for (uint32_t p : rest) {
+            if (qlen[p] && tlen[p]) cand.push_back(p);
+            else units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
+        }
+        auto key = [&](uint32_t p) { return ((uint64_t)n_passes(qlen[p]) << 4) | (qlen[p] & 15u); };
+        std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) {
+            if (key(a) != key(b)) return key(a) < key(b);
+            if (qlen[a] != qlen[b]) return qlen[a] > qlen[b];
+            return tlen[a] > tlen[b];
+        });
+        for (size_t i = 0; i < cand.size();) {
+            const uint32_t A = cand[i];
+            if (i + 1 < cand.size() && key(cand[i + 1]) == key(A) && n_passes(qlen[A]) < 64) {
+                const uint32_t B = cand[i + 1];
+                const uint64_t M = std::max(tlen[A], tlen[B]);
+                const uint64_t wave = (uint64_t)qlen[A] * M;
+                const uint64_t useful = (uint64_t)qlen[A] * tlen[A] + (uint64_t)qlen[B] * tlen[B];
+                if (4 * useful >= 3 * 2 * wave) {  // waste <= 25 %
+                    units.push_back({2, A, B, wave});
+                    i += 2;
+                    continue;
+                }
+            }
+            // a long pair without a partner is coupled with itself: one wave per pass
+            const uint32_t ps = n_passes(qlen[A]);
+            units.push_back({ps >= 4 && ps < 64 ? 2 : 0, A, A, (uint64_t)qlen[A] * tlen[A]});
+            ++i;
+        }
+    } else {
+        for (uint32_t p : rest) units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
+    }
+    std::stable_sort(units.begin(), units.end(), [](const Unit& x, const Unit& y) { return x.cost > y.cost; });
+    pl.order.reserve(n_pairs);
+    Plan::Chunk cur{};
+    uint32_t couples_before = 0;
+    auto open_chunk = [&]() {
+        cur = Plan::Chunk{(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0,
+                          (uint32_t)(pl.duals.size() / 2), 0, (uint32_t)(pl.flexes.size() / 2), 0,
+                          couples_before, 0, 0};
+    };
+    open_chunk();
+    for (const Unit& u : units) {
+        const uint32_t na = qlen[u.a], ma = tlen[u.a], nb = qlen[u.b], mb = tlen[u.b];
+        const bool two = u.kind && u.a != u.b;
+        const uint64_t pd = !want_cigar ? 0 : ptr_dwords(na, ma) + (two ? ptr_dwords(nb, mb) : 0);
+        if (cur.count && cur.ptr_dwords + pd > budget_dw) {
+            pl.chunks.push_back(cur);
+            open_chunk();
+        }
+        const uint32_t q[2] = {u.a, u.b};
+        for (int h = 0; h < (two ? 2 : 1); ++h) {
+            const uint32_t x = q[h];
+            pl.ptr_off[x] = cur.ptr_dwords;
+            pl.bnd_off[x] = cur.bnd_words;
+            const uint64_t xd = want_cigar ? ptr_dwords(qlen[x], tlen[x]) : 0;
+            // flex: pair A holds both pairs' absolute int32 boundary rows, interleaved;
+            // each pair keeps a region of its own for the int32 fallback ('-' in a query)
+            uint64_t bw = bnd_words(qlen[x], tlen[x]);
+            if (u.kind == 2 && h == 0 && n_passes(na) > 1)
+                bw = std::max<uint64_t>(bw, 8ull * ((uint64_t)std::max(ma, mb) + 1));
+            bw += bw & 1;  // keep every region 8-byte aligned (64-bit hand-off records)
+            cur.ptr_dwords += xd;
+            cur.bnd_words += bw;
+            pl.order.push_back(x);
+        }
+        if (u.kind == 1) {
+            pl.duals.push_back(u.a);
+            pl.duals.push_back(u.b);
+            ++cur.dcount;
+        } else if (u.kind == 2) {
+            pl.flexes.push_back(u.a);
+            pl.flexes.push_back(u.b);
+            ++cur.fcount;
+        } else {
+            pl.singles.push_back(u.a);
+            ++cur.scount;
+        }
+        if (u.kind) {
+            pl.n_dual_pairs += 2;
+            ++couples_before;
+        }
+        cur.count += two ? 2 : 1;
+    }
+    if (cur.count) pl.chunks.push_back(cur);
+    // A fill kernel that walks its own pair only pays when nothing else of the
+    // chunk runs in the separate traceback kernel anyway.
+    pl.fused = want_cigar && pl.n_dual_pairs == 0 && !(flags & kPlanUnfused);
+    pl.flex_task_off.assign(1, 0);
+    for (size_t w = 0; w < pl.flexes.size() / 2; ++w)
+        pl.flex_task_off.push_back(pl.flex_task_off.back() + n_passes(qlen[pl.flexes[2 * w]]));
+    pl.flex_tasks.assign(pl.flex_task_off.back(), 0u);
+    for (const auto& ch : pl.chunks) {
+        uint32_t at = pl.flex_task_off[ch.fbegin], maxp = 0;
+        for (uint32_t w = ch.fbegin; w < ch.fbegin + ch.fcount; ++w)
+            maxp = std::max(maxp, pl.flex_task_off[w + 1] - pl.flex_task_off[w]);
+        for (uint32_t ps = 0; ps < maxp; ++ps)
+            for (uint32_t w = ch.fbegin; w < ch.fbegin + ch.fcount; ++w)
+                if (pl.flex_task_off[w + 1] - pl.flex_task_off[w] > ps) pl.flex_tasks[at++] = w * 64u + ps;
+    }
+    for (const auto& c : pl.chunks) {
+        pl.ws_ptr_dwords = std::max(pl.ws_ptr_dwords, c.ptr_dwords);
+        pl.ws_bnd_words = std::max(pl.ws_bnd_words, c.bnd_words);
+    }
+}
+
+void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
+                       int match, int mismatch, int gap_open, int gap_extend, bool want_cigar, uint64_t budget,
+                       uint32_t flags) {
+    pl = AffinePlan{};
+    pl.n_pairs = n_pairs;
+    pl.type = type;
+    pl.match = match;
+    pl.mismatch = mismatch;
+    pl.open = gap_open;
+    pl.extend = gap_extend;
+    pl.want_cigar = want_cigar;
+    pl.qlen.assign(qlen, qlen + n_pairs);
+    pl.tlen.assign(tlen, tlen + n_pairs);
+    const std::vector<uint32_t> byc = by_cells(n_pairs, qlen, tlen);
+    // units: couples of equal shape for the packed fill (global / semi, values
+    // within int16), else single pairs
+    const bool dual_ok = !(flags & kPlanInt32Only);
+    std::vector<std::pair<uint32_t, uint32_t>> units;  // (a, b); b == UINT32_MAX: single
+    units.reserve(n_pairs);
+    for (uint32_t k = 0; k < n_pairs;) {
+        const uint32_t x = byc[k];
+        if (dual_ok && k + 1 < n_pairs && qlen[byc[k + 1]] == qlen[x] && tlen[byc[k + 1]] == tlen[x] &&
+            affine_fits_int16(type, qlen[x], tlen[x], match, mismatch, gap_open, gap_extend)) {
+            units.push_back({x, byc[k + 1]});
+            k += 2;
+        } else {
+            units.push_back({x, UINT32_MAX});
+            ++k;
+        }
+    }
+    pl.slot_off = slot_offsets(n_pairs, qlen, tlen, &pl.slots_bytes);
+    const uint64_t budget_entries = std::max<uint64_t>(budget / 8, 1);
+    pl.ptr_off.assign(n_pairs, 0);
+    pl.bnd_off.assign(n_pairs, 0);
+    AffinePlan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0};
+    for (const auto& u : units) {
+        const uint32_t ids[2] = {u.first, u.second};
+        const int cnt = u.second == UINT32_MAX ? 1 : 2;
+        uint64_t pe = 0;
+        for (int h = 0; h < cnt; ++h) pe += want_cigar ? ptr_dwords(qlen[ids[h]], tlen[ids[h]]) : 0;
+        if (c.count && c.ptr_entries + pe > budget_entries) {
+            pl.chunks.push_back(c);
+            c = {(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0, (uint32_t)(pl.duals.size() / 2), 0, 0, 0};
+        }
+        for (int h = 0; h < cnt; ++h) {
+            const uint32_t p = ids[h];
+            pl.ptr_off[p] = c.ptr_entries;
+            pl.bnd_off[p] = c.bnd_entries;
+            c.ptr_entries += want_cigar ? ptr_dwords(qlen[p], tlen[p]) : 0;
+            c.bnd_entries += bnd_words(qlen[p], tlen[p]);
+            pl.order.push_back(p);
+            ++c.count;
+        }
+        if (cnt == 2) {
+            pl.duals.push_back(u.first);
+            pl.duals.push_back(u.second);
+            ++c.dcount;
+        } else {
+            pl.singles.push_back(u.first);
+            ++c.scount;
+        }
+    }
+    if (c.count) pl.chunks.push_back(c);
+    for (const auto& ch : pl.chunks) {
+        pl.ws_ptr_entries = std::max(pl.ws_ptr_entries, ch.ptr_entries);
+        pl.ws_bnd_entries = std::max(pl.ws_bnd_entries, ch.bnd_entries);
+    }
+}
+
+}  // namespace ta

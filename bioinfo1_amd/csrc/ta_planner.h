@@ -1,0 +1,99 @@
+// bioinfo1_amd/csrc/ta_planner.h -- host planning of a batch (no HIP):
+// which kernel each pair runs in, the visit order, the chunks the 2-bit
+// traceback-code workspace is cut into, and every per-pair offset the kernels
+// read.  The device side (ta_api.hip / ta_affine.hip) uploads the arrays
+// packed into one block and launches per chunk.  Pure C++ so that it builds
+// with g++ for the CPU tests and the ASan/UBSan/TSan runs (tests/test_host_sanitizers.py).
+#pragma once
+
+#include <stdint.h>
+
+#include <vector>
+
+#include "ta_layout.h"
+
+namespace ta {
+
+// Plan flags (include/team_align_c.h TA_PLAN_*): which kernels may be used.
+constexpr uint32_t kPlanInt32Only = 1u;  // no packed two-pair kernels
+constexpr uint32_t kPlanNoFlex = 2u;     // no rebased (different-shape) couples
+constexpr uint32_t kPlanUnfused = 4u;    // int32-only plans: traceback as its own kernel
+
+// Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
+bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
+// Scoring whose rebased 16-bit values cannot overflow in the flexible fill (ta_flex.hip).
+bool flex_fits(int mode, int match, int mismatch, int gap);
+// Every packed value of the affine dual fill (ta_affine.hip) within int16.
+bool affine_fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int open, int ext);
+
+// Linear-gap plan (team::Align scoring).
+struct Plan {
+    uint32_t n_pairs = 0;
+    int type = 0, match = 0, mismatch = 0, gap = 0;
+    bool want_cigar = false;
+    bool wide = false;   // local mode with |values| that could reach 2^25: unscaled int32 kernel
+    bool fused = false;  // int32-only plans: the fill kernel walks its own pair
+    std::vector<uint32_t> qlen, tlen;
+    std::vector<uint32_t> order;    // traceback order (all pairs)
+    std::vector<uint32_t> singles;  // int32 fill: pair ids
+    std::vector<uint32_t> duals;    // equal-shape couples: 2 pair ids each
+    std::vector<uint32_t> flexes;   // different-shape couples: 2 pair ids each
+    // per flex couple: first task (one per query pass); last entry = total tasks
+    std::vector<uint32_t> flex_task_off;
+    // per chunk, the chunk's flex tasks in ticket order (couple * 64 + pass),
+    // pass-major: every couple's pass 0, then every pass 1, ...
+    std::vector<uint32_t> flex_tasks;
+    std::vector<uint64_t> ptr_off, bnd_off, slot_off;
+    struct Chunk {
+        uint32_t begin, count;    // all pairs (traceback order)
+        uint32_t sbegin, scount;  // int32 fill: pairs
+        uint32_t dbegin, dcount;  // dual fill: pair couples
+        uint32_t fbegin, fcount;  // flexible dual fill: pair couples
+        uint32_t cbegin;          // couples (dual + flex) before this chunk: its slice of the hand-back list
+        uint64_t ptr_dwords, bnd_words;
+    };
+    std::vector<Chunk> chunks;
+    uint32_t n_dual_pairs = 0;  // pairs in packed couples (dual + flex)
+    uint64_t slots_bytes = 0, ws_ptr_dwords = 0, ws_bnd_words = 0;
+};
+
+// Plans n_pairs pairs; budget = bytes of 2-bit codes per chunk (> 0).
+void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type, int match,
+                int mismatch, int gap, bool want_cigar, uint64_t budget, uint32_t flags);
+
+// Affine-gap plan (the extension of include/team_align_c.h).
+struct AffinePlan {
+    uint32_t n_pairs = 0;
+    int type = 0, match = 0, mismatch = 0, open = 0, extend = 0;
+    bool want_cigar = false;
+    std::vector<uint32_t> qlen, tlen;
+    std::vector<uint32_t> order;           // pairs by descending cells: the big ones start first
+    std::vector<uint32_t> singles, duals;  // int32 fill: pairs; packed fill: 2 pair ids per couple
+    std::vector<uint64_t> ptr_off, bnd_off, slot_off;
+    struct Chunk {
+        uint32_t begin, count;    // plan order (traceback)
+        uint32_t sbegin, scount;  // singles
+        uint32_t dbegin, dcount;  // couples
+        uint64_t ptr_entries, bnd_entries;
+    };
+    std::vector<Chunk> chunks;
+    uint64_t slots_bytes = 0, ws_ptr_entries = 0, ws_bnd_entries = 0;
+};
+
+// budget = bytes of 4-bit codes (8-byte entries) per chunk (> 0).
+void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
+                       int match, int mismatch, int gap_open, int gap_extend, bool want_cigar, uint64_t budget,
+                       uint32_t flags);
+
+// One contiguous block holding several arrays, each at a 256-byte aligned
+// offset: the plan's per-pair arrays go to the device in one copy.
+struct BlockLayout {
+    uint64_t bytes = 0;
+    uint64_t add(uint64_t n_bytes) {
+        const uint64_t at = bytes;
+        bytes += (n_bytes + 255) & ~uint64_t(255);
+        return at;
+    }
+};
+
+}  // namespace ta

@@ -18,15 +18,20 @@
 
 namespace {
 
-// One context (device stream + staging buffers) per calling thread: Align is
-// re-entrant in the reference and the mapper calls it from OpenMP threads.
+// One context (device stream + grow-only device and pinned staging buffers)
+// per calling thread: Align is re-entrant in the reference and the mapper
+// calls it from OpenMP threads.  After the first calls a call allocates
+// nothing: one pinned upload, the fill kernel (which walks its own pair),
+// one download, one synchronisation (ta_host_batch.h).
 struct ThreadCtx {
     ta_context* ctx = nullptr;
+    std::vector<char> arena;  // CIGAR bytes of the last call (grow-only)
     ~ThreadCtx() { ta_context_destroy(ctx); }
 };
 
+thread_local ThreadCtx tc;
+
 ta_context* thread_context() {
-    thread_local ThreadCtx tc;
     if (!tc.ctx) {
         int r = ta_context_create(0, &tc.ctx);
         if (r != TA_OK) throw std::runtime_error("team::Align: no usable gfx950 GPU (" + std::string(ta_status_string(r)) + ")");
@@ -48,7 +53,8 @@ int Align(const char* query, unsigned int query_len, const char* target, unsigne
     const uint32_t ql = query_len, tl = target_len;
     int32_t score = 0;
     uint32_t tb = 0;
-    std::vector<char> arena(cigar ? ta_cigar_slot_bytes(ql, tl) : 0);
+    std::vector<char>& arena = tc.arena;
+    if (cigar && arena.size() < ta_cigar_slot_bytes(ql, tl)) arena.resize(ta_cigar_slot_bytes(ql, tl));
     uint64_t coff = 0;
     uint32_t clen = 0;
     int r = ta_align_batch(ctx, 1, query, &qoff, &ql, target, &toff, &tl, t, match, mismatch, gap, cigar != nullptr,

@@ -307,8 +307,12 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
     const uint32_t P = (uint32_t)pair_read.size();
     if (!P) return TM_OK;
     ta_plan* plan = nullptr;
+    // the mapper owns the device: its code workspace may take most of the free
+    // HBM (fewer, fuller chunks for long reads; the library default is half, <= 64 GiB)
+    size_t free_b = 0, total_b = 0;
+    const uint64_t budget = hipMemGetInfo(&free_b, &total_b) == hipSuccess ? (uint64_t)free_b / 100 * 85 : 0;
     int rc = ta_plan_create(ctx->ta, P, ql.data(), tl.data(), opt->type, opt->match, opt->mismatch, opt->gap,
-                            opt->want_cigar, 0, &plan);
+                            opt->want_cigar, budget, 0, &plan);
     if (rc != TA_OK) return fail(ctx, rc == TA_ERR_BAD_TYPE ? TM_ERR_BAD_TYPE : TM_ERR_DEVICE,
                                  std::string("ta_plan_create: ") + ta_last_error(ctx->ta));
     const uint64_t slots = ta_plan_cigar_slots_bytes(plan);

@@ -115,7 +115,13 @@ def related_batch(n_pairs: int, qlen: int, tlen: int, seed: int = 0x5EED, rate: 
     """Config-2 "related" variant: target = query with ``rate`` substitutions,
     insertions and deletions each, trimmed / padded (random bases) to tlen.
     Per pair the stream yields qlen query bases, then 2 draws per query base
-    (event, base), then tlen padding bases."""
+    (event, base), then tlen padding bases.  (related_batch_torch makes the
+    same bytes on the GPU, for config 5's 100k pairs.)"""
+    block = max(1, (64 << 20) // (8 * (3 * qlen + tlen) + 1))  # bound the draw matrix to ~64 MB
+    if n_pairs > block:
+        parts = [related_batch(min(block, n_pairs - k), qlen, tlen, seed, rate, first_pair + k)
+                 for k in range(0, n_pairs, block)]
+        return _concat(parts)
     d = draws(seed, n_pairs, qlen + 2 * qlen + tlen, first_pair)
     top = (d >> np.uint64(62)).astype(np.intp)
     q = ACGT[top[:, :qlen]]
@@ -147,6 +153,88 @@ def related_batch(n_pairs: int, qlen: int, tlen: int, seed: int = 0x5EED, rate: 
     qoff = np.arange(n_pairs, dtype=np.uint64) * np.uint64(qlen)
     toff = np.arange(n_pairs, dtype=np.uint64) * np.uint64(tlen)
     return PairBatch(qf, qoff, np.full(n_pairs, qlen, np.uint32), t, toff, np.full(n_pairs, tlen, np.uint32))
+
+
+def _concat(parts) -> PairBatch:
+    qb = np.concatenate([b.qbytes for b in parts])
+    tb = np.concatenate([b.tbytes for b in parts])
+    ql = np.concatenate([b.qlen for b in parts])
+    tl = np.concatenate([b.tlen for b in parts])
+    qoff = np.zeros(ql.shape[0], np.uint64)
+    toff = np.zeros(tl.shape[0], np.uint64)
+    if ql.shape[0]:
+        qoff[1:] = np.cumsum(ql[:-1], dtype=np.uint64)
+        toff[1:] = np.cumsum(tl[:-1], dtype=np.uint64)
+    return PairBatch(qb, qoff, ql, tb, toff, tl)
+
+
+# --- the same generators on the GPU (torch int64, two's-complement wrap) ----
+
+def _i64(x: int) -> int:
+    return x - (1 << 64) if x >= 1 << 63 else x
+
+
+def _torch_mix(z):
+    """splitmix64's output mix on an int64 tensor (logical shifts by masking)."""
+    import torch
+
+    def shr(v, k):
+        return (v >> k) & ((1 << (64 - k)) - 1)
+
+    z = (z ^ shr(z, 30)) * _i64(int(_M1))
+    z = (z ^ shr(z, 27)) * _i64(int(_M2))
+    return z ^ shr(z, 31)
+
+
+def draws_torch(seed: int, n_pairs: int, count: int, first_pair: int, device):
+    """``draws`` on ``device`` as int64 (bit patterns of the uint64 outputs)."""
+    import torch
+
+    st = torch.arange(first_pair, first_pair + n_pairs, dtype=torch.int64, device=device) ^ _i64(seed)
+    k = torch.arange(1, count + 1, dtype=torch.int64, device=device) * _i64(int(_GOLDEN))
+    return _torch_mix(st[:, None] + k[None, :])
+
+
+def related_batch_torch(n_pairs: int, qlen: int, tlen: int, seed: int = 0x5EED, rate: float = 0.05,
+                        first_pair: int = 0, device="cuda", block: int = 256):
+    """related_batch generated on the GPU: returns (query bytes, target bytes)
+    as uint8 device tensors [n_pairs * qlen], [n_pairs * tlen] -- the pairs
+    of a fixed-shape batch back to back (offsets p*qlen, p*tlen), the same
+    bytes as related_batch (tests/test_synth.py)."""
+    import torch
+
+    acgt = torch.tensor(list(b"ACGT"), dtype=torch.uint8, device=device)
+    Q = torch.empty(n_pairs * qlen, dtype=torch.uint8, device=device)
+    T = torch.empty(n_pairs * tlen, dtype=torch.uint8, device=device)
+    W = max(2 * qlen, tlen)
+    for k0 in range(0, n_pairs, block):
+        B = min(block, n_pairs - k0)
+        d = draws_torch(seed, B, 3 * qlen + tlen, first_pair + k0, device)
+        top = ((d >> 62) & 3).long()
+        q = acgt[top[:, :qlen]]
+        ev = ((d[:, qlen:3 * qlen:2] >> 11) & ((1 << 53) - 1)).double() * (1.0 / 2**53)
+        eb = acgt[top[:, qlen + 1:3 * qlen:2]]
+        pad = acgt[top[:, 3 * qlen:]]
+        del d, top
+        sub = ev < rate
+        ins = (ev >= rate) & (ev < 2 * rate)
+        dele = (ev >= 2 * rate) & (ev < 3 * rate)
+        base = torch.where(sub, eb, q)
+        emit_base = ~dele
+        cnt = ins.long() + emit_base.long()
+        pos = torch.cumsum(cnt, 1) - cnt
+        L = cnt.sum(1)
+        seq = torch.zeros((B, W), dtype=torch.uint8, device=device)
+        rows = torch.arange(B, device=device)[:, None].expand(B, qlen)
+        seq[rows[ins], pos[ins]] = eb[ins]
+        pb = pos + ins.long()
+        seq[rows[emit_base], pb[emit_base]] = base[emit_base]
+        col = torch.arange(tlen, device=device)[None, :]
+        padded = torch.gather(pad, 1, (col - L[:, None]).clamp(min=0))
+        t = torch.where(col < L[:, None], seq[:, :tlen], padded)
+        Q[k0 * qlen:(k0 + B) * qlen] = q.reshape(-1)
+        T[k0 * tlen:(k0 + B) * tlen] = t.reshape(-1)
+    return Q, T
 
 
 def ragged_batch(n_pairs: int, min_len: int, max_len: int, seed: int = 0x5EED, alphabet: bytes = b"ACGT",

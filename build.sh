@@ -29,6 +29,8 @@ done
 "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_affine.hip" -o "$B/ta_affine.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip" -o "$B/ta_api.o" & pids+=($!)
 "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp" -o "$B/shim.o" & pids+=($!)
+# host planner: plain C++ (also built with g++ under ASan/UBSan/TSan by tests/test_host_sanitizers.py)
+g++ -O2 -std=c++17 -fPIC -Wall -c "$CS/ta_planner.cpp" -o "$B/ta_planner.o" & pids+=($!)
 # mapper stages (libteam_mapper.so) and the team_mapper_amd CLI
 for f in tm_minimizers tm_match tm_chain; do
   "$HIPCC" "${FLAGS[@]}" -c "$CS/$f.hip" -o "$B/$f.o" & pids+=($!)
@@ -38,11 +40,15 @@ for f in tm_api tm_fastx; do
 done
 "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp" -o "$B/tm_main.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/shim.o" -o "$OUT"
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_planner.o" "$B/shim.o" \
+  -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$OUT"
 PKG="$ROOT/bioinfo1_amd"
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/tm_{minimizers,match,chain,api,fastx}.o -L"$PKG" -lteam_alignment -lz \
   -Wl,-rpath,'$ORIGIN' -o "$PKG/libteam_mapper.so"
 "$HIPCC" --offload-arch=gfx950 "$B/tm_main.o" -L"$PKG" -lteam_mapper -lteam_alignment -Wl,-rpath,'$ORIGIN' \
   -o "$PKG/team_mapper_amd"
+# the drop-in single-call measurement (bench.py --workload dropin), our side
+g++ -std=c++17 -O3 -pthread -I"$ROOT/include" "$ROOT/scripts/dropin_bench.cpp" -L"$PKG" -lteam_alignment \
+  -Wl,-rpath,"$PKG" -Wl,-rpath,'$ORIGIN/../bioinfo1_amd' -o "$B/dropin_amd"
 make -s -C "$ROOT/oracle" >/dev/null
 echo "built $OUT"

@@ -54,6 +54,10 @@ const char* ta_last_error(const ta_context* ctx);
  * calling thread so concurrent callers (team_mapper.cpp:596 OpenMP) are safe. */
 int ta_context_create(int device, ta_context** out);
 void ta_context_destroy(ta_context* ctx);
+/* Free the context's cached device workspace and staging buffers (they are
+ * grow-only: a large batch keeps its traceback-code workspace for the next
+ * one).  Waits for the context's last execution.  The context stays usable. */
+void ta_context_release(ta_context* ctx);
 
 /* Bytes of the per-pair CIGAR slot for an n x m pair: 2*(n+m)+2, an upper
  * bound on any run-length CIGAR of that pair (team_alignment.cpp:145-160). */
@@ -71,6 +75,11 @@ uint64_t ta_cigar_slot_bytes(uint32_t query_len, uint32_t target_len);
  * cigar_arena[cigar_off[p] .. cigar_off[p]+cigar_len[p]).
  * want_cigar == 0 is the reference's cigar == nullptr mode: no traceback.
  * Returns TA_ERR_BAD_TYPE for an unknown type (no pair is computed).
+ * No device allocation per call once the context's grow-only buffers fit the
+ * batch: per call one pinned upload of the plan arrays, offsets and (up to
+ * 4 MB) sequences, the kernels, the downloads, one or two synchronisations.
+ * Caller buffers may be pageable or pinned (pinned ones, e.g. allocated with
+ * hipHostMalloc, transfer at full PCIe rate).
  */
 int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, const uint64_t* query_off,
                    const uint32_t* query_len, const char* target_bytes, const uint64_t* target_off,
@@ -83,11 +92,16 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, c
  * benchmark path).  A plan fixes the lengths (host arrays, copied) and the
  * scoring, lays out the device workspace (2-bit traceback pointers, pass
  * boundary rows) and chunks the batch when the pointer matrices exceed
- * workspace_budget bytes (0 = library default).
+ * workspace_budget bytes (0 = library default: half the free HBM, at most
+ * 64 GiB).  flags: 0, or TA_PLAN_* below (kernel selection for tests and
+ * measurements; results are identical either way).
  */
+#define TA_PLAN_INT32_ONLY 1u /* no packed two-pairs-per-wave int16 kernels */
+#define TA_PLAN_NO_FLEX 2u    /* no rebased couples of different shapes */
+#define TA_PLAN_UNFUSED 4u    /* int32-only plans: traceback as its own kernel, not inside the fill */
 int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
                    const uint32_t* target_len_host, int type, int match, int mismatch, int gap, int want_cigar,
-                   uint64_t workspace_budget, ta_plan** out);
+                   uint64_t workspace_budget, uint32_t flags, ta_plan** out);
 void ta_plan_destroy(ta_plan* plan);
 /* Total bytes of the device CIGAR slot arena the caller must provide. */
 uint64_t ta_plan_cigar_slots_bytes(const ta_plan* plan);
@@ -101,6 +115,8 @@ uint32_t ta_plan_chunks(const ta_plan* plan);
 uint32_t ta_plan_dual_pairs(const ta_plan* plan);
 /* Of those, the pairs in couples of different shapes / beyond int16 (ta_flex.hip). */
 uint32_t ta_plan_flex_pairs(const ta_plan* plan);
+/* 1 when the fill kernel walks its own pair (int32-only plans with CIGAR on). */
+int ta_plan_fused(const ta_plan* plan);
 
 /* Device pointers for one execution of a plan. */
 typedef struct ta_device_io {
@@ -116,18 +132,10 @@ typedef struct ta_device_io {
 } ta_device_io;
 
 /* Enqueue the whole batch on `hip_stream` (a hipStream_t; NULL = the HIP
- * null stream, as everywhere in HIP).  Asynchronous: returns after enqueueing. */
+ * null stream, as everywhere in HIP).  Asynchronous: returns after enqueueing.
+ * Plans of one context share its workspace: an execution on a different
+ * stream than the context's previous one waits for that one first. */
 int ta_plan_execute(ta_plan* plan, const ta_device_io* io, void* hip_stream);
-
-/* Enqueue n_batches executions of the plan, batch b with ios[b] (same
- * lengths and scoring; e.g. a mapper's successive read chunks), pipelined:
- * batch b's traceback runs on an internal stream beside batch b+1's fill,
- * with the traceback codes double-buffered (when two code workspaces fit in
- * HBM; else the batches run one after the other).  Every batch's results are
- * complete when hip_stream reaches the end of the enqueued work.  Per batch
- * the results are exactly ta_plan_execute's.  No reference counterpart: the
- * reference aligns one pair per team::Align call (team_mapper.cpp:666-678). */
-int ta_plan_execute_batches(ta_plan* plan, const ta_device_io* ios, uint32_t n_batches, void* hip_stream);
 
 /* After the plan's executions have completed (stream synchronised): TA_OK, or
  * TA_ERR_DEVICE when a kernel reported an internal failure since the last
@@ -139,6 +147,15 @@ int ta_plan_check(ta_plan* plan);
  * workspace) or only the traceback, for profiling the two kernels. */
 int ta_plan_execute_fill(ta_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
 int ta_plan_execute_traceback(ta_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
+
+/* Pack n_pairs CIGARs from their slots (device: cigar_slots, cigar_start,
+ * cigar_len as written by an execution) back to back into dst (device):
+ * pair p's bytes go to dst[dst_off[p] ..).  Enqueued on hip_stream.  For a
+ * caller that gathers CIGAR bytes between GPUs (bench.py's RCCL gather) or
+ * downloads them.  The reference has no counterpart (one std::string per
+ * team::Align call, team_alignment.cpp:160). */
+int ta_compact_cigars(ta_context* ctx, uint32_t n_pairs, const char* cigar_slots, const uint64_t* cigar_start,
+                      const uint32_t* cigar_len, const uint64_t* dst_off, char* dst, void* hip_stream);
 
 /*
  * ---- Affine-gap extension (BASELINE config 5: "affine gaps + full CIGAR
@@ -159,10 +176,12 @@ int ta_plan_execute_traceback(ta_plan* plan, const ta_device_io* io, void* hip_s
 typedef struct ta_affine_plan ta_affine_plan;
 
 /* As ta_plan_create, with the affine scoring.  Traceback codes take 4 bits per
- * cell (source M/I/D/STOP + the E and F extension bits). */
+ * cell (source M/I/D/STOP + the E and F extension bits).  flags:
+ * TA_PLAN_INT32_ONLY or 0. */
 int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
                           const uint32_t* target_len_host, int type, int match, int mismatch, int gap_open,
-                          int gap_extend, int want_cigar, uint64_t workspace_budget, ta_affine_plan** out);
+                          int gap_extend, int want_cigar, uint64_t workspace_budget, uint32_t flags,
+                          ta_affine_plan** out);
 void ta_affine_plan_destroy(ta_affine_plan* plan);
 uint64_t ta_affine_plan_cigar_slots_bytes(const ta_affine_plan* plan);
 uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* plan);

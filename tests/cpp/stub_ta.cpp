@@ -1,0 +1,71 @@
+// tests/cpp/stub_ta.cpp -- a CPU stand-in for the part of the C ABI
+// (include/team_align_c.h) that the drop-in team::Align shim calls, backed by
+// the oracle (oracle/align_oracle.c).  Only for the ThreadSanitizer run of
+// the shim (tests/test_host_sanitizers.py): the shim's per-thread contexts
+// and buffers are exercised from many threads without a GPU.  Never part of
+// the product (which has no CPU path).
+#include <cstring>
+#include <string>
+
+#include "team_align_c.h"
+
+extern "C" int oracle_align(const char* q, unsigned n, const char* t, unsigned m, int type, int match, int mismatch,
+                            int gap, int want_cigar, int* score_out, unsigned* target_begin_out, char* cigar_out,
+                            size_t cigar_cap, size_t* cigar_len);
+
+struct ta_context {
+    std::string last_error;
+    int device = 0;
+};
+
+extern "C" {
+
+const char* ta_status_string(int status) {
+    switch (status) {
+        case TA_OK: return "ok";
+        case TA_ERR_BAD_TYPE: return "Unknown AlignmentType provided.";
+        case TA_ERR_CIGAR: return "Unknown error in determining cigar string.";
+        default: return "error";
+    }
+}
+
+const char* ta_last_error(const ta_context* ctx) { return ctx ? ctx->last_error.c_str() : ""; }
+
+int ta_context_create(int device, ta_context** out) {
+    *out = new ta_context();
+    (*out)->device = device;
+    return TA_OK;
+}
+
+void ta_context_destroy(ta_context* ctx) { delete ctx; }
+
+uint64_t ta_cigar_slot_bytes(uint32_t n, uint32_t m) { return 2ull * ((uint64_t)n + m) + 2; }
+
+int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff, const uint32_t* qlen,
+                   const char* tb, const uint64_t* toff, const uint32_t* tlen, int type, int match, int mismatch,
+                   int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* arena, uint64_t arena_bytes,
+                   uint64_t* cigar_off, uint32_t* cigar_len) {
+    uint64_t at = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        int s = 0;
+        unsigned b = 0;
+        size_t cl = 0;
+        const int r = oracle_align(qb + qoff[p], qlen[p], tb + toff[p], tlen[p], type, match, mismatch, gap,
+                                   want_cigar, &s, &b, want_cigar ? arena + at : nullptr,
+                                   want_cigar ? arena_bytes - at : 0, &cl);
+        if (r) {
+            ctx->last_error = ta_status_string(r);
+            return r;
+        }
+        if (score) score[p] = s;
+        if (target_begin) target_begin[p] = b;
+        if (want_cigar) {
+            cigar_off[p] = at;
+            cigar_len[p] = (uint32_t)cl;
+            at += cl;
+        }
+    }
+    return TA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,105 @@
+"""bench.py's multi-rank result gather on CPU: world-size 2
+and 3 gloo groups run bench.ResultGather over several steps of stand-in
+plans (host tensors, ragged per-rank pair counts and CIGAR sizes); rank 0's
+gathered records and CIGAR bytes must be the rank-ordered concatenation of
+what every rank produced in the last step.  The GPU run of the same path
+(bench.py --gpus 2, 2 ranks on one device) is tests/test_bench_gpu.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+class _FakeDist:
+    def __init__(self, dist, world, rank):
+        self.dist, self.world, self.rank = dist, world, rank
+        self.backend = "gloo"
+        self.dev = torch.device("cpu")
+        self.cdev = self.dev
+
+    def all_gather_flat(self, out, t, async_op):
+        parts = list(out.chunk(self.world))
+        return self.dist.all_gather(parts, t, async_op=async_op)
+
+
+class _FakePlan:
+    """What ResultGather reads from a DevicePlan, for one rank and one step."""
+
+    def __init__(self, rank, step, n):
+        rng = np.random.default_rng(1000 * rank + step)
+        self.P = n
+        self.score = torch.from_numpy(rng.integers(-50, 50, n).astype(np.int32))
+        self.target_begin = torch.from_numpy(rng.integers(0, 9, n).astype(np.int32))
+        lens = rng.integers(1, 40, n).astype(np.int32)
+        self.cigar_len = torch.from_numpy(lens)
+        self.cig = [bytes(rng.integers(48, 90, int(k)).astype(np.uint8)) for k in lens]
+
+    def compact_cigars(self):
+        allb = b"".join(self.cig)
+        dst = torch.zeros(len(allb) + 37, dtype=torch.uint8)  # slack: slots are larger than the CIGARs
+        dst[:len(allb)] = torch.frombuffer(bytearray(allb), dtype=torch.uint8)
+        off = torch.zeros(self.P + 1, dtype=torch.int64)
+        off[1:] = torch.cumsum(self.cigar_len.to(torch.int64), 0)
+        return dst, off
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    import bench
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sizes = [7, 3, 11][:world]
+    g = bench.ResultGather(_FakeDist(dist, world, rank), max(sizes), True)
+    for step in range(4):
+        g.post(_FakePlan(rank, step, sizes[rank]))
+        g.clear_old()
+    g.drain()
+    if rank == 0:
+        sc, tb, cl, cig = g.last()
+        q.put((sc.tolist(), tb.tolist(), cl.tolist(), cig))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_result_gather_rank_order(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sizes = [7, 3, 11][:world]
+    plans = [_FakePlan(r, 3, sizes[r]) for r in range(world)]
+    assert got[0] == sum((p.score.tolist() for p in plans), [])
+    assert got[1] == sum((p.target_begin.tolist() for p in plans), [])
+    assert got[2] == sum((p.cigar_len.tolist() for p in plans), [])
+    assert got[3] == b"".join(b"".join(p.cig) for p in plans)
+
+
+def test_bench_refuses_world_mismatch():
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 3 and "WORLD_SIZE=1 but --gpus 2" in r.stderr

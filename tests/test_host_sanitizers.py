@@ -1,0 +1,111 @@
+"""The build's host code under the CPU sanitizers (race
+detection / sanitizers).  Built here with g++/gcc, no GPU:
+
+* ASan + UBSan: the oracle (align_oracle.c, affine_oracle.c) on every golden
+  case, the host planner (ta_planner.cpp) on random batches, the FASTA/FASTQ
+  reader (tm_fastx.cpp) on the committed mapper inputs (plain and gzip);
+* TSan: the planner from 8 threads at once, and the drop-in team::Align shim
+  (team_alignment_shim.cpp: per-thread contexts and buffers) called from 4
+  threads, its C ABI stood in for by the oracle (tests/cpp/stub_ta.cpp)."""
+import gzip
+import json
+import os
+import shutil
+import subprocess
+
+import pytest
+from conftest import GOLDEN, ROOT
+
+CS = os.path.join(ROOT, "bioinfo1_amd", "csrc")
+OUT = os.path.join(ROOT, "build", "san")
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=1",
+           UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1", TSAN_OPTIONS="halt_on_error=1")
+
+
+def _build(name, san, extra_c=(), extra_cpp=(), libs=()):
+    os.makedirs(OUT, exist_ok=True)
+    exe = os.path.join(OUT, name)
+    objs = []
+    for c in extra_c:  # C sources compiled as C (without OpenMP: the sanitizers do not model it)
+        o = os.path.join(OUT, f"{name}_{os.path.basename(c)}.o")
+        subprocess.check_call(["gcc", "-std=c11", "-O1", "-g", san, "-c", c, "-o", o])
+        objs.append(o)
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-g", san, "-pthread", "-I", os.path.join(ROOT, "include"),
+                           *extra_cpp, *objs, "-o", exe, *libs])
+    return exe
+
+
+def _cases_file():
+    path = os.path.join(OUT, "cases.txt")
+    with open(path, "w") as f:
+        for name in ("kat.json", "random_pairs.json"):
+            with open(os.path.join(GOLDEN, name)) as g:
+                for c in json.load(g)["cases"]:
+                    want = "ERR - -" if c["error"] else f"{c['score']} {c['target_begin']} {c['cigar'] or '-'}"
+                    f.write(f"{c['type']} {c['match']} {c['mismatch']} {c['gap']} {c['query'] or '-'} "
+                            f"{c['target'] or '-'} {want}\n")
+    return path
+
+
+@pytest.fixture(scope="module")
+def asan_driver():
+    return _build("driver_asan", "-fsanitize=address,undefined",
+                  extra_c=[os.path.join(ROOT, "oracle", "align_oracle.c"),
+                           os.path.join(ROOT, "oracle", "affine_oracle.c")],
+                  extra_cpp=[os.path.join(ROOT, "tests", "cpp", "sanitize_driver.cpp"),
+                             os.path.join(CS, "ta_planner.cpp"), os.path.join(CS, "tm_fastx.cpp")], libs=["-lz"])
+
+
+def _run(cmd, timeout=600):
+    r = subprocess.run(cmd, capture_output=True, text=True, env=ENV, timeout=timeout)
+    assert r.returncode == 0 and "Sanitizer" not in r.stderr and "runtime error" not in r.stderr, \
+        (r.stdout[-2000:], r.stderr[-4000:])
+    return r.stdout
+
+
+def test_oracle_asan_ubsan(asan_driver):
+    out = _run([asan_driver, "oracle", _cases_file()])
+    assert "fails 0" in out and int(out.split("cases ")[1].split()[0]) >= 690
+
+
+def test_planner_asan_ubsan(asan_driver):
+    assert "fails 0" in _run([asan_driver, "planner", "12345", "150", "1"])
+
+
+def test_fastx_asan_ubsan(asan_driver):
+    mdir = os.path.join(GOLDEN, "mapper")
+    gz = os.path.join(OUT, "r60k.fastq.gz")
+    with open(os.path.join(mdir, "r60k.fastq"), "rb") as f, gzip.open(gz, "wb") as g:
+        shutil.copyfileobj(f, g)
+    outs = {}
+    for path, fq in ((os.path.join(mdir, "g60k.fasta"), 0), (os.path.join(mdir, "demo_reads.fasta"), 0),
+                     (os.path.join(mdir, "r60k.fastq"), 1), (gz, 1), (os.path.join(mdir, "rrep.fastq"), 1),
+                     (os.path.join(mdir, "demo.fasta"), 1)):  # the last: FASTA read as FASTQ -> clean refusal
+        outs[path] = _run([asan_driver, "fastx", path, str(fq)])
+    assert outs[gz] == outs[os.path.join(mdir, "r60k.fastq")]  # gzip and plain parse alike
+    assert "records" in outs[os.path.join(mdir, "g60k.fasta")]
+
+
+def test_planner_tsan():
+    exe = _build("driver_tsan", "-fsanitize=thread",
+                 extra_c=[os.path.join(ROOT, "oracle", "align_oracle.c"), os.path.join(ROOT, "oracle", "affine_oracle.c")],
+                 extra_cpp=[os.path.join(ROOT, "tests", "cpp", "sanitize_driver.cpp"),
+                            os.path.join(CS, "ta_planner.cpp"), os.path.join(CS, "tm_fastx.cpp")], libs=["-lz"])
+    assert "fails 0" in _run([exe, "planner", "777", "40", "8"])
+
+
+def test_dropin_shim_tsan(kat_cases, random_cases):
+    """team::Align's shim from 4 threads (the mapper's OpenMP loop) under TSan."""
+    exe = _build("shim_tsan", "-fsanitize=thread",
+                 extra_c=[os.path.join(ROOT, "oracle", "align_oracle.c")],
+                 extra_cpp=[os.path.join(ROOT, "tests", "cpp", "shim_caller.cpp"),
+                            os.path.join(CS, "team_alignment_shim.cpp"), os.path.join(ROOT, "tests", "cpp", "stub_ta.cpp")])
+    cases = kat_cases + random_cases[:120]
+    lines = [f"{c['type']} {c['match']} {c['mismatch']} {c['gap']} {c['query'] or '-'} {c['target'] or '-'}"
+             for c in cases]
+    want = [f"ERR {c['error']}" if c["error"] else f"{c['score']} {c['target_begin']} {c['cigar'] or '-'}"
+            for c in cases]
+    r = subprocess.run([exe, "threads"], input="\n".join(lines) + "\n", capture_output=True, text=True, env=ENV,
+                       timeout=600)
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr, r.stderr[-4000:]
+    assert r.stdout.splitlines() == want

@@ -36,3 +36,20 @@ def test_ragged_and_from_pairs():
     assert all(0 <= int(x) <= 30 for x in b.qlen)
     s = b.slice(3, 7)
     assert [s.query(k) for k in range(4)] == [b.query(3 + k) for k in range(4)]
+
+
+def test_related_batch_blocked_is_prefix_stable():
+    # the blocked generator gives the same pairs as one block
+    a = synth.related_batch(5, 300, 280, seed=11)
+    b = synth.related_batch(3, 300, 280, seed=11, first_pair=2)
+    assert [a.target(2 + k) for k in range(3)] == [b.target(k) for k in range(3)]
+
+
+def test_related_batch_torch_matches_numpy():
+    import torch
+
+    for (P, n, m, first) in ((7, 300, 280, 0), (5, 200, 450, 3), (3, 64, 64, 11)):
+        want = synth.related_batch(P, n, m, seed=0x5EED, first_pair=first)
+        q, t = synth.related_batch_torch(P, n, m, seed=0x5EED, first_pair=first, device="cpu", block=2)
+        assert q.numpy().tobytes() == want.qbytes.tobytes()
+        assert t.numpy().tobytes() == want.tbytes.tobytes()
