@@ -1048,7 +1048,7 @@ int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qle
     auto* pl = new ta_affine_plan();
     pl->ctx = ctx;
     ta::build_affine_plan(pl->h, n_pairs, qlen, tlen, type, match, mismatch, gap_open, gap_extend, want_cigar != 0,
-                          budget ? budget : ta_host::default_budget(ctx), flags);
+                          budget ? budget : ta_host::default_budget(ctx), flags, 4 * ctx->cu_count);
     ta::BlockLayout L;
     AffOffs o = aff_layout(pl->h, L);
     const uint64_t upload = L.bytes;
@@ -1109,7 +1109,8 @@ int ta_align_batch_affine(ta_context* ctx, uint32_t n_pairs, const char* qb, con
     ta_affine_plan pl;
     pl.ctx = ctx;
     ta::build_affine_plan(pl.h, n_pairs, qlen, tlen, type, match, mismatch, gap_open, gap_extend, want_cigar != 0,
-                          ta_host::batch_budget(ctx, n_pairs, qlen, tlen, want_cigar, sizeof(uint2)), 0);
+                          ta_host::batch_budget(ctx, n_pairs, qlen, tlen, want_cigar, sizeof(uint2)), 0,
+                          4 * ctx->cu_count);
     AffineHostPlan hp(&pl);
     return ta_host::host_batch(ctx, hp, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, qend, tend, want_cigar, score,
                                target_begin, arena, arena_bytes, cigar_off, cigar_len);

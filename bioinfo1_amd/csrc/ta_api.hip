@@ -390,7 +390,7 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
     auto* pl = new ta_plan();
     pl->ctx = ctx;
     ta::build_plan(pl->h, n_pairs, qlen, tlen, type, match, mismatch, gap, want_cigar != 0,
-                   budget ? budget : ta_host::default_budget(ctx), flags);
+                   budget ? budget : ta_host::default_budget(ctx), flags, 4 * ctx->cu_count);
     // all per-pair arrays in one device allocation, uploaded in one copy
     ta::BlockLayout L;
     PlanOffs o = layout_uploaded(pl->h, L);
@@ -474,7 +474,7 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
     ta_plan pl;
     pl.ctx = ctx;
     ta::build_plan(pl.h, n_pairs, qlen, tlen, type, match, mismatch, gap, want_cigar != 0,
-                   ta_host::batch_budget(ctx, n_pairs, qlen, tlen, want_cigar, 4), 0);
+                   ta_host::batch_budget(ctx, n_pairs, qlen, tlen, want_cigar, 4), 0, 4 * ctx->cu_count);
     LinearHostPlan hp(&pl);
     return ta_host::host_batch(ctx, hp, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, qend, tend, want_cigar, score,
                                target_begin, arena, arena_bytes, cigar_off, cigar_len);

@@ -5,6 +5,7 @@
 
 #include <algorithm>
 #include <cstdlib>
+#include <functional>
 #include <numeric>
 
 namespace ta {
@@ -86,10 +87,44 @@ std::vector<uint64_t> slot_offsets(uint32_t n_pairs, const uint32_t* qlen, const
     return off;
 }
 
+// Chunk boundaries over units in launch order: a chunk closes when the next
+// unit's codes would exceed the budget.  A chunk closed by the budget is then
+// trimmed to a whole number of "rounds" -- multiples of wave_quantum waves (one
+// wave per SIMD) -- when it holds at least one: the fill is VALU-bound, so a
+// chunk takes as long as its busiest SIMD, and 2,500 waves on 1,024 SIMDs
+// (3 on some, 2 on others) run at 2.44 / 3 of the rate of 2,048 (config 5
+// affine: 100k pairs in 20 chunks of 5,000 vs 25 of 4,096).
+std::vector<size_t> chunk_starts(size_t n_units, uint64_t budget, uint32_t wave_quantum,
+                                 const std::function<uint64_t(size_t)>& codes,
+                                 const std::function<uint64_t(size_t)>& waves) {
+    std::vector<size_t> starts;
+    size_t k = 0;
+    while (k < n_units) {
+        const size_t start = k;
+        uint64_t used = 0, w = 0;
+        while (k < n_units) {
+            const uint64_t c = codes(k);
+            if (k > start && used + c > budget) break;
+            used += c;
+            w += waves(k);
+            ++k;
+        }
+        if (k < n_units && wave_quantum && w >= wave_quantum) {
+            const uint64_t target = w / wave_quantum * wave_quantum;
+            while (w > target && k > start + 1) {
+                --k;
+                w -= waves(k);
+            }
+        }
+        starts.push_back(start);
+    }
+    return starts;
+}
+
 }  // namespace
 
 void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type, int match,
-                int mismatch, int gap, bool want_cigar, uint64_t budget, uint32_t flags) {
+                int mismatch, int gap, bool want_cigar, uint64_t budget, uint32_t flags, uint32_t wave_quantum) {
     pl = Plan{};
     pl.n_pairs = n_pairs;
     pl.type = type;
@@ -174,6 +209,17 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         for (uint32_t p : rest) units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
     }
     std::stable_sort(units.begin(), units.end(), [](const Unit& x, const Unit& y) { return x.cost > y.cost; });
+    auto unit_codes = [&](size_t k) -> uint64_t {
+        const Unit& u = units[k];
+        if (!want_cigar) return 0;
+        return ptr_dwords(qlen[u.a], tlen[u.a]) + (u.kind && u.a != u.b ? ptr_dwords(qlen[u.b], tlen[u.b]) : 0);
+    };
+    auto unit_waves = [&](size_t k) -> uint64_t {
+        const Unit& u = units[k];
+        return u.kind == 2 ? n_passes(qlen[u.a]) : 1;  // flex: one wave per (couple, pass)
+    };
+    const std::vector<size_t> starts = chunk_starts(units.size(), budget_dw, wave_quantum, unit_codes, unit_waves);
+    size_t next_cut = 1;
     pl.order.reserve(n_pairs);
     Plan::Chunk cur{};
     uint32_t couples_before = 0;
@@ -183,13 +229,14 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
                           couples_before, 0, 0};
     };
     open_chunk();
-    for (const Unit& u : units) {
-        const uint32_t na = qlen[u.a], ma = tlen[u.a], nb = qlen[u.b], mb = tlen[u.b];
+    for (size_t k = 0; k < units.size(); ++k) {
+        const Unit& u = units[k];
+        const uint32_t na = qlen[u.a], ma = tlen[u.a], mb = tlen[u.b];
         const bool two = u.kind && u.a != u.b;
-        const uint64_t pd = !want_cigar ? 0 : ptr_dwords(na, ma) + (two ? ptr_dwords(nb, mb) : 0);
-        if (cur.count && cur.ptr_dwords + pd > budget_dw) {
+        if (next_cut < starts.size() && k == starts[next_cut]) {
             pl.chunks.push_back(cur);
             open_chunk();
+            ++next_cut;
         }
         const uint32_t q[2] = {u.a, u.b};
         for (int h = 0; h < (two ? 2 : 1); ++h) {
@@ -249,7 +296,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
 
 void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
                        int match, int mismatch, int gap_open, int gap_extend, bool want_cigar, uint64_t budget,
-                       uint32_t flags) {
+                       uint32_t flags, uint32_t wave_quantum) {
     pl = AffinePlan{};
     pl.n_pairs = n_pairs;
     pl.type = type;
@@ -282,14 +329,23 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
     pl.ptr_off.assign(n_pairs, 0);
     pl.bnd_off.assign(n_pairs, 0);
     AffinePlan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0};
-    for (const auto& u : units) {
+    auto unit_codes = [&](size_t k) -> uint64_t {
+        const auto& u = units[k];
+        if (!want_cigar) return 0;
+        return ptr_dwords(qlen[u.first], tlen[u.first]) +
+               (u.second == UINT32_MAX ? 0 : ptr_dwords(qlen[u.second], tlen[u.second]));
+    };
+    const std::vector<size_t> starts =
+        chunk_starts(units.size(), budget_entries, wave_quantum, unit_codes, [](size_t) -> uint64_t { return 1; });
+    size_t next_cut = 1;
+    for (size_t k = 0; k < units.size(); ++k) {
+        const auto& u = units[k];
         const uint32_t ids[2] = {u.first, u.second};
         const int cnt = u.second == UINT32_MAX ? 1 : 2;
-        uint64_t pe = 0;
-        for (int h = 0; h < cnt; ++h) pe += want_cigar ? ptr_dwords(qlen[ids[h]], tlen[ids[h]]) : 0;
-        if (c.count && c.ptr_entries + pe > budget_entries) {
+        if (next_cut < starts.size() && k == starts[next_cut]) {
             pl.chunks.push_back(c);
             c = {(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0, (uint32_t)(pl.duals.size() / 2), 0, 0, 0};
+            ++next_cut;
         }
         for (int h = 0; h < cnt; ++h) {
             const uint32_t p = ids[h];

@@ -57,9 +57,10 @@ struct Plan {
     uint64_t slots_bytes = 0, ws_ptr_dwords = 0, ws_bnd_words = 0;
 };
 
-// Plans n_pairs pairs; budget = bytes of 2-bit codes per chunk (> 0).
+// Plans n_pairs pairs; budget = bytes of 2-bit codes per chunk (> 0);
+// wave_quantum = the device's SIMD count (0: no rounding of chunk sizes).
 void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type, int match,
-                int mismatch, int gap, bool want_cigar, uint64_t budget, uint32_t flags);
+                int mismatch, int gap, bool want_cigar, uint64_t budget, uint32_t flags, uint32_t wave_quantum = 0);
 
 // Affine-gap plan (the extension of include/team_align_c.h).
 struct AffinePlan {
@@ -83,7 +84,7 @@ struct AffinePlan {
 // budget = bytes of 4-bit codes (8-byte entries) per chunk (> 0).
 void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type,
                        int match, int mismatch, int gap_open, int gap_extend, bool want_cigar, uint64_t budget,
-                       uint32_t flags);
+                       uint32_t flags, uint32_t wave_quantum = 0);
 
 // One contiguous block holding several arrays, each at a 256-byte aligned
 // offset: the plan's per-pair arrays go to the device in one copy.

@@ -204,10 +204,11 @@ void plan_worker(uint64_t seed, int iters) {
         const uint32_t flags = (uint32_t)(splitmix(s) % 8);
         const bool cig = splitmix(s) % 4 != 0;
         ta::Plan pl;
-        ta::build_plan(pl, P, q.data(), t.data(), type, ma, mi, g, cig, budget, flags);
+        const uint32_t quantum = (splitmix(s) & 1) ? 1024u : (uint32_t)(splitmix(s) % 9);
+        ta::build_plan(pl, P, q.data(), t.data(), type, ma, mi, g, cig, budget, flags, quantum);
         check_linear(pl, budget);
         ta::AffinePlan ap;
-        ta::build_affine_plan(ap, P, q.data(), t.data(), type, ma, mi, -2, g, cig, budget, flags & 1u);
+        ta::build_affine_plan(ap, P, q.data(), t.data(), type, ma, mi, -2, g, cig, budget, flags & 1u, quantum);
         check_affine(ap);
     }
 }
