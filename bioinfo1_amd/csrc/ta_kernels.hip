@@ -471,6 +471,8 @@ hipError_t launch_flex(int mode, bool cigar, const FillArgs& a, hipStream_t s) {
     switch (mode * 2 + (cigar ? 1 : 0)) {
         case 0: return launch_flex_mode<kGlobal, false>(a, s);
         case 1: return launch_flex_mode<kGlobal, true>(a, s);
+        case 2: return launch_flex_mode<kLocal, false>(a, s);
+        case 3: return launch_flex_mode<kLocal, true>(a, s);
         case 4: return launch_flex_mode<kSemi, false>(a, s);
         case 5: return launch_flex_mode<kSemi, true>(a, s);
         default: return hipErrorInvalidValue;

@@ -13,10 +13,21 @@ namespace ta {
 // The flexible fill keeps V = S - O within a wave's span: 1,024 rows + 2 x 64
 // columns of cells whose neighbours differ by at most |score| + |gap| <= 2*mag
 // (plus the 64-step drift between rebases).
+// Local mode also ranks a column's 16 rows by 16 * (V_r - V_0) + 15 - r,
+// within 16 * 15 * 2 * mag.
 bool flex_fits(int mode, int ma, int mi, int gap) {
-    if (mode == kLocal) return false;
+    (void)mode;
     const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
     return (kPassRows + 3LL * kWave) * 2 * mag * 2 <= 30000;
+}
+
+// Local mode: the values a wave holds are H - ma*j - O, H in [0, Hmax], so the
+// largest score of the pair bounds them (and the clamp base -ma*j - O).
+bool flex_local_fits(uint32_t n, uint32_t m, int ma, int mi, int gap) {
+    const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
+    const long long hmax = (long long)std::min(n, m) * std::max({0LL, (long long)ma, (long long)mi}) +
+                           ((long long)n + m) * std::max(0LL, (long long)gap);
+    return hmax + 3LL * kWave * std::llabs(ma) + 8 * mag <= 30000;
 }
 
 // Bounds of the biased 16-bit values of ta_dual.hip (S and every candidate),
@@ -178,8 +189,10 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         // lane), neighbours by (n, m), at most 25 % of the wave's cells wasted
         std::vector<uint32_t> cand;
         for (uint32_t p : rest) {
-            if (qlen[p] && tlen[p]) cand.push_back(p);
-            else units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
+            if (qlen[p] && tlen[p] && (type != kLocal || flex_local_fits(qlen[p], tlen[p], match, mismatch, gap)))
+                cand.push_back(p);
+            else
+                units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
         }
         auto key = [&](uint32_t p) { return ((uint64_t)n_passes(qlen[p]) << 4) | (qlen[p] & 15u); };
         std::stable_sort(cand.begin(), cand.end(), [&](uint32_t a, uint32_t b) {

@@ -23,6 +23,8 @@ constexpr uint32_t kPlanUnfused = 4u;    // int32-only plans: traceback as its o
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
 // Scoring whose rebased 16-bit values cannot overflow in the flexible fill (ta_flex.hip).
 bool flex_fits(int mode, int match, int mismatch, int gap);
+// ... and, local mode, a pair whose scores stay within its int16 range.
+bool flex_local_fits(uint32_t n, uint32_t m, int match, int mismatch, int gap);
 // Every packed value of the affine dual fill (ta_affine.hip) within int16.
 bool affine_fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int open, int ext);
 

@@ -19,7 +19,7 @@ for m in 0 1 2; do
     "$HIPCC" "${FLAGS[@]}" -DTA_DUAL_MODE=$m -DTA_DUAL_CIGAR=$c -c "$CS/ta_dual.hip" -o "$B/ta_dual_$m$c.o" & pids+=($!)
   done
 done
-for m in 0 2; do
+for m in 0 1 2; do
   for c in 0 1; do
     "$HIPCC" "${FLAGS[@]}" -DTA_FLEX_MODE=$m -DTA_FLEX_CIGAR=$c -c "$CS/ta_flex.hip" -o "$B/ta_flex_$m$c.o" & pids+=($!)
   done
@@ -40,7 +40,7 @@ for f in tm_api tm_fastx; do
 done
 "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp" -o "$B/tm_main.o" & pids+=($!)
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_planner.o" "$B/shim.o" \
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_planner.o" "$B/shim.o" \
   -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$OUT"
 PKG="$ROOT/bioinfo1_amd"
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/tm_{minimizers,match,chain,api,fastx}.o -L"$PKG" -lteam_alignment -lz \

@@ -284,6 +284,15 @@ FLEX_FUZZ = [
     (0, (1, -1, -1), b"ACGT", 10700, 11200, 4, False, False),
     (2, (1, -1, -1), b"ACGT", 4100, 6000, 3, False, False),     # odd groups: long singles coupled with themselves
     (0, (2, -3, -2), b"ACGT", 4100, 6000, 5, True, True),
+    # local mode (clamp, row-major first-max argmax, cost-tracking walk)
+    (1, (1, -1, -1), b"ACGT", 1, 300, 120, False, False),
+    (1, (2, -3, -2), b"ACGT", 900, 2200, 24, True, False),
+    (1, (2, -3, -2), b"ACGT", 900, 2200, 24, True, True),      # '-' in queries: handed to the int32 fill
+    (1, (3, -2, 0), b"ACGTN", 1000, 1100, 16, False, False),   # gap 0
+    (1, (2, -1, 2), b"AC", 500, 1500, 20, False, False),       # positive gap
+    (1, (1, -1, -1), b"ACGT", 10700, 12500, 6, False, False),  # long: rebasing, 11+ passes
+    (1, (1, -1, -1), b"ACGT", 4100, 6000, 3, False, False),    # odd group: long singles coupled with themselves
+    (1, (5, -4, -3), b"ACGT", 1000, 3000, 12, False, False),
 ]
 
 
@@ -436,3 +445,27 @@ def test_plans_on_two_streams(aligner, oracle):
         np.testing.assert_array_equal(r.scores, want.scores)
         assert r.cigars() == want.cigars()
         p.close()
+
+
+def test_flex_local_no_positive_cell(aligner, oracle):
+    """Local mode where no cell is positive (all mismatches): score 0, CIGAR
+    "1\0", target_begin 2 -- the first cell in row-major order -- through the
+    flexible fill's argmax (ragged shapes, several passes)."""
+    rng = np.random.default_rng(0x0C)
+    qa, ta = np.frombuffer(b"AC", np.uint8), np.frombuffer(b"GT", np.uint8)
+    pairs = []
+    for k in range(12):  # couples: same pass count and n mod 16, different m
+        n0 = int(rng.integers(40, 2600))
+        for h in range(2):
+            n = n0 - 16 * h
+            m = int(rng.integers(max(1, n0 * 8 // 10), n0 * 12 // 10 + 1))
+            pairs.append((qa[rng.integers(2, size=n)].tobytes(), ta[rng.integers(2, size=m)].tobytes()))
+    b = synth.from_pairs(pairs)
+    plan = DevicePlan(aligner, b, 1, 1, -1, -1, True)
+    assert plan.flex_pairs >= 12, plan.flex_pairs
+    plan.close()
+    want = oracle.align_batch(b, 1, 1, -1, -1, True)
+    got = run_plan(aligner, b, 1, (1, -1, -1), True)
+    np.testing.assert_array_equal(got.scores, want.scores)
+    np.testing.assert_array_equal(got.target_begins, want.target_begins)
+    assert got.cigars() == want.cigars()
