@@ -389,6 +389,8 @@ def digest_name(args, n_pairs):
         return ("cfg2_related_local" if args.related else "cfg2_local"), 10000
     if args.workload in ("cfg3", "cfg4") and (args.mode, args.scoring) == ("semiGlobal", "1,-1,-1") and n_pairs >= 64:
         return "cfg3_semi_sample", 64
+    if args.workload in ("cfg3", "cfg4") and (args.mode, args.scoring) == ("local", "1,-1,-1") and n_pairs >= 64:
+        return "cfg3_local_sample", 64
     if args.workload == "cfg5" and (args.mode, args.scoring) == ("semiGlobal", "1,-1,-1") and n_pairs >= 32:
         return "cfg5_semi_sample", 32
     return None, 0
@@ -556,7 +558,8 @@ def main_align(args, D):
         alg = fill_alg_bytes(batch, cigar, affine)
         achieved = alg / (fill_ms / 1e3) / 1e9
         tag = (f"{args.mode}_{'cigar' if cigar else 'score'}_{args.pairs}x{args.qlen}x{args.tlen}"
-               if args.workload not in ("cfg3", "cfg4") else f"cfg3_{'cigar' if cigar else 'score'}_{plan.P}")
+               if args.workload not in ("cfg3", "cfg4")
+               else f"cfg3_{'' if args.mode == 'semiGlobal' else args.mode + '_'}{'cigar' if cigar else 'score'}_{plan.P}")
         if affine:
             tag = "affine_" + tag
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -564,7 +567,11 @@ def main_align(args, D):
                 "traffic_source": "rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE of this command, per fill launch "
                                   "(profiles/traffic.json; scripts/profile.sh)",
                 "kernel": dominant_kernel(plan, mode, cigar, affine), "kernel_ms": round(fill_ms, 4),
+                "launches_per_step": plan.chunks,
+                "kernel_ms_per_dispatch": round(fill_ms / max(plan.chunks, 1), 4),
                 "alg_bytes_per_launch": alg,
+                "per_launch_note": "one launch = the step's fill dispatches (one per chunk); traffic and "
+                                   "ops/cell are rocprof per-dispatch averages x launches_per_step",
                 "note": "integer DP: VALU-bound, not HBM- or MFMA-bound (see valu)"}
         ops = load_profile("valu.json", tag)
         valu = {"kernel_gcups": round(batch.cells / (fill_ms / 1e3) / 1e9, 2),
@@ -742,6 +749,7 @@ def main_mapper(args, D):
     for _ in range(args.steps):
         r = step()
         st, cells = mp.stage_times()
+        plan_stats = mp.align_plan_stats()
         for k, v in st.items():
             stages[k] = stages.get(k, 0.0) + v / args.steps
     torch.cuda.synchronize(D.dev)
@@ -766,6 +774,7 @@ def main_mapper(args, D):
                                       f"of per-read records and CIGAR bytes"},
             "reads_mapped": int(r.mapped.sum()), "reads_per_s": round(args.pairs * D.world / (ms / 1e3), 1),
             "index_build_s": round(index_s, 3), "stage_ms": {k: round(v, 3) for k, v in stages.items()},
+            "align_plan": plan_stats,
             "roofline": None, "device": torch.cuda.get_device_name(D.dev), **extra,
         }
     idx.close()

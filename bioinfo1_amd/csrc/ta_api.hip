@@ -362,6 +362,13 @@ void ta_context_release(ta_context* ctx) {
     for (auto* b : {&ctx->pin_in, &ctx->pin_out}) ta_host::release(*b, true);
 }
 
+uint64_t ta_context_held_bytes(const ta_context* ctx) {
+    if (!ctx) return 0;
+    uint64_t n = 0;
+    for (const auto* b : {&ctx->blk, &ctx->out, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd}) n += b->cap;
+    return n;
+}
+
 void ta_context_destroy(ta_context* ctx) {
     if (!ctx) return;
     ta_context_release(ctx);

@@ -308,9 +308,13 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
     if (!P) return TM_OK;
     ta_plan* plan = nullptr;
     // the mapper owns the device: its code workspace may take most of the free
-    // HBM (fewer, fuller chunks for long reads; the library default is half, <= 64 GiB)
+    // HBM (fewer, fuller chunks for long reads; the library default is half,
+    // <= 64 GiB).  Memory the alignment context already holds from the last
+    // batch is reused, so it counts as free.
     size_t free_b = 0, total_b = 0;
-    const uint64_t budget = hipMemGetInfo(&free_b, &total_b) == hipSuccess ? (uint64_t)free_b / 100 * 85 : 0;
+    const uint64_t budget = hipMemGetInfo(&free_b, &total_b) == hipSuccess
+                                ? ((uint64_t)free_b + ta_context_held_bytes(ctx->ta)) / 100 * 85
+                                : 0;
     int rc = ta_plan_create(ctx->ta, P, ql.data(), tl.data(), opt->type, opt->match, opt->mismatch, opt->gap,
                             opt->want_cigar, budget, 0, &plan);
     if (rc != TA_OK) return fail(ctx, rc == TA_ERR_BAD_TYPE ? TM_ERR_BAD_TYPE : TM_ERR_DEVICE,
@@ -369,6 +373,11 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
         }
         return TM_OK;
     };
+    ctx->plan_stats[0] = P;
+    ctx->plan_stats[1] = ta_plan_chunks(plan);
+    ctx->plan_stats[2] = ta_plan_dual_pairs(plan);
+    ctx->plan_stats[3] = ta_plan_flex_pairs(plan);
+    ctx->plan_stats[4] = ta_plan_workspace_bytes(plan);
     rc = run();
     ta_plan_destroy(plan);
     if (rc == TM_OK) rc = stage(6);
@@ -381,6 +390,12 @@ int tm_stage_times(const tm_context* ctx, double* ms, uint32_t n, uint64_t* alig
     if (!ctx || (n && !ms)) return TM_ERR_ARG;
     for (uint32_t i = 0; i < n && i < (uint32_t)tmap::kStages; ++i) ms[i] = ctx->stage_ms[i];
     if (aligned_cells) *aligned_cells = ctx->stage_cells;
+    return TM_OK;
+}
+
+int tm_align_plan_stats(const tm_context* ctx, uint64_t out[5]) {
+    if (!ctx || !out) return TM_ERR_ARG;
+    for (int i = 0; i < 5; ++i) out[i] = ctx->plan_stats[i];
     return TM_OK;
 }
 

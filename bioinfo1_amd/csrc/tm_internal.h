@@ -93,6 +93,7 @@ struct tm_context {
     tmap::DevBuf m_qoff, m_toff, m_score, m_tb, m_slots, m_cstart, m_clen, m_coff, m_cdst;
     double stage_ms[tmap::kStages] = {};
     uint64_t stage_cells = 0;
+    uint64_t plan_stats[5] = {};  // tm_align_plan_stats
 };
 
 namespace tmap {

@@ -31,7 +31,7 @@ TM_OK = 0
 # Every symbol include/team_mapper_c.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = ["tm_status_string", "tm_last_error", "tm_context_create", "tm_context_destroy", "tm_minimizer_bound",
                "tm_minimize_batch", "tm_chain_batch", "tm_index_create", "tm_index_destroy", "tm_index_stats",
-               "tm_map_batch", "tm_stage_times", "tm_map_files"]
+               "tm_map_batch", "tm_stage_times", "tm_align_plan_stats", "tm_map_files"]
 
 _lib = None
 
@@ -76,6 +76,7 @@ def lib() -> C.CDLL:
     L.tm_map_batch.argtypes = [vp, vp, C.c_uint32, vp, u64p, u32p, C.POINTER(Options), u8p, u8p, u32p, u32p, u32p,
                                u32p, i32p, vp, C.c_uint64, u64p, u32p]
     L.tm_stage_times.argtypes = [vp, C.POINTER(C.c_double), C.c_uint32, u64p]
+    L.tm_align_plan_stats.argtypes = [vp, u64p]
     L.tm_map_files.argtypes = [C.c_char_p, C.c_char_p, C.POINTER(Options), C.c_char_p, C.c_int]
     _lib = L
     return L
@@ -154,6 +155,12 @@ class Mapper:
         cells = C.c_uint64()
         _check(lib().tm_stage_times(self._h, ms, 8, C.byref(cells)))
         return dict(zip(self.STAGES, list(ms))), cells.value
+
+    def align_plan_stats(self):
+        """The alignment plan of the last map_batch (ta_plan_* counts)."""
+        out = (C.c_uint64 * 5)()
+        _check(lib().tm_align_plan_stats(self._h, out))
+        return dict(zip(["pairs", "chunks", "dual_pairs", "flex_pairs", "workspace_bytes"], list(out)))
 
     # -- chaining -----------------------------------------------------------
     def chain_batch(self, lists):

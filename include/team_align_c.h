@@ -59,6 +59,12 @@ void ta_context_destroy(ta_context* ctx);
  * one).  Waits for the context's last execution.  The context stays usable. */
 void ta_context_release(ta_context* ctx);
 
+/* Device bytes the context currently holds in its grow-only buffers (the
+ * code workspace and staging).  A caller sizing ta_plan_create's workspace
+ * budget from hipMemGetInfo adds this back: the free figure does not count
+ * memory the context will reuse. */
+uint64_t ta_context_held_bytes(const ta_context* ctx);
+
 /* Bytes of the per-pair CIGAR slot for an n x m pair: 2*(n+m)+2, an upper
  * bound on any run-length CIGAR of that pair (team_alignment.cpp:145-160). */
 uint64_t ta_cigar_slot_bytes(uint32_t query_len, uint32_t target_len);

@@ -122,6 +122,11 @@ int tm_map_batch(tm_context* ctx, const tm_index* idx, uint32_t n_reads, const c
  * covered.  Stages are separated by stream synchronisations. */
 int tm_stage_times(const tm_context* ctx, double* ms, uint32_t n, uint64_t* aligned_cells);
 
+/* The alignment plan of the last tm_map_batch: out[0] pairs, [1] chunks,
+ * [2] pairs on the packed int16 fills (dual + flexible), [3] pairs on the
+ * flexible fill, [4] code workspace bytes (ta_plan_* of libteam_alignment). */
+int tm_align_plan_stats(const tm_context* ctx, uint64_t out[5]);
+
 /*
  * The whole mapper on files (the reference's main, team_mapper.cpp:319-796):
  * reference FASTA (first record) and reads (FASTQ, else FASTA; plain or

@@ -40,6 +40,16 @@ def pmc_avgs(d):
     return {k: {c: sum(v) / len(v) for c, v in cs.items()} for k, cs in acc.items()}
 
 
+def bench_line(d):
+    for name in ("prof_trace.log", "prof_sq.log"):
+        p = os.path.join(d, name)
+        if os.path.exists(p):
+            for ln in open(p):
+                if ln.startswith("{"):
+                    return json.loads(ln)
+    return None
+
+
 def main():
     src, rtag, wtag = sys.argv[1], sys.argv[2], sys.argv[3]
     prof = os.path.join(ROOT, "profiles")
@@ -58,22 +68,24 @@ def main():
         # the dominant fill launch (dual and int32 fills both match; the int32
         # one may be the near-empty fallback launch for '-' queries)
         k, cs = max(fill.items(), key=lambda kv: kv[1].get("SQ_INSTS_VALU", 0))
+        bl = bench_line(src)
+        # per-dispatch averages x dispatches per step = the step's fill (every
+        # step repeats the same chunk dispatches)
+        per_step = bl.get("chunks", 1) if bl else 1
         tr = None
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
-            tr = int((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024)
+            tr = int((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024 * per_step)
         p = os.path.join(prof, "traffic.json")
         d = json.load(open(p)) if os.path.exists(p) else {}
         d[wtag] = tr
         json.dump(d, open(p, "w"), indent=1)
         if "SQ_INSTS_VALU" in cs:
-            # SQ_INSTS_VALU counts wave-instructions; cells per launch from the workload tag
-            parts = wtag.split("_")[-1].split("x")
-            cells = int(parts[0]) * int(parts[1]) * int(parts[2])
-            waves = cs.get("SQ_WAVES", 0)
+            # SQ_INSTS_VALU counts wave-instructions; cells per step from the bench line
+            cells = bl["config"]["cells_per_gpu"]
             # per lane-cell: wave-instr x 64 lanes / cells
             p = os.path.join(prof, "valu.json")
             d = json.load(open(p)) if os.path.exists(p) else {}
-            d[wtag] = round(cs["SQ_INSTS_VALU"] * 64 / cells, 3)
+            d[wtag] = round(cs["SQ_INSTS_VALU"] * 64 * per_step / cells, 3)
             json.dump(d, open(p, "w"), indent=1)
         print(k, json.dumps(cs, indent=1))
     print("summary written to", prof)

@@ -40,12 +40,13 @@ def digest_batch(name):
         "ragged_global": lambda: synth.ragged_batch(2000, 0, 3000, 0xF00D),
         "cfg5_semi_sample": lambda: synth.related_batch(32, 10000, 10000, 0x5EED),
         "cfg3_semi_sample": lambda: synth.cfg3_batch(64)[0],
+        "cfg3_local_sample": lambda: synth.cfg3_batch(64)[0],
     }
     return spec[name]()
 
 
 DIGESTS = ["cfg2_local", "cfg2_related_local", "g1k_global", "s1k_semi", "ragged_local", "ragged_semi",
-           "ragged_global", "cfg5_semi_sample", "cfg3_semi_sample"]
+           "ragged_global", "cfg5_semi_sample", "cfg3_semi_sample", "cfg3_local_sample"]
 
 
 def cigar_digest(res, P):

@@ -233,8 +233,15 @@ def _cfg3_sample(ref):
                 "synth.cfg3_batch() vs their true-origin windows, semiGlobal 1/-1/-1")
 
 
+def _cfg3_local_sample(ref):
+    b, _, _ = synth.cfg3_batch(64)
+    make_digest(ref, "cfg3_local_sample", b, 1, 1, -1, -1,
+                "config 3 stand-in sample, local: first 64 ONT-like reads (1-20 kb, 10% error, 50% reverse) of "
+                "synth.cfg3_batch() vs their true-origin windows, local 1/-1/-1")
+
+
 # digests added after the first set (regenerate one with --only NAME)
-DIGEST_SPECS = {"cfg3_semi_sample": _cfg3_sample}
+DIGEST_SPECS = {"cfg3_semi_sample": _cfg3_sample, "cfg3_local_sample": _cfg3_local_sample}
 
 
 if __name__ == "__main__":

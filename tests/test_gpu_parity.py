@@ -234,6 +234,19 @@ def test_config3_full_batch_properties(aligner):
     np.testing.assert_array_equal(r.cigar_lens[:64], d["cigar_lens"])
 
 
+def test_config3_local_full_batch_properties(aligner):
+    """The config 3 stand-in in local mode (the flexible packed fill's local
+    path): every CIGAR is a local path scoring the reported score, score-only
+    agrees, and the first 64 pairs are bit-exact against the reference digest
+    (test_digest[cfg3_local_sample])."""
+    b, _, _ = synth.cfg3_batch(10000)
+    r = _check_full(aligner, b, 1, (1, -1, -1))
+    meta, d = load_digest("cfg3_local_sample")
+    np.testing.assert_array_equal(r.scores[:64], d["scores"])
+    np.testing.assert_array_equal(r.target_begins[:64], d["target_begins"])
+    np.testing.assert_array_equal(r.cigar_lens[:64], d["cigar_lens"])
+
+
 def test_config5_shape_properties(aligner):
     """Config 5 shape (10 kb x 10 kb semi-global, linear gap) on 512 pairs:
     path/score properties; the first 32 pairs bit-exact vs the reference digest."""
