@@ -40,11 +40,16 @@ struct DualIo {
 };
 
 // One pass of both pairs; see run_pass (ta_kernels.hip) for the shared structure.
-template <int MODE, bool CIGAR, int NV>
+// M3 (local only): every value carries the offset `off` (local_max3_offset)
+// so that the clamp folds into a three-input max and the stripe's row max is
+// a tree of three-input maxima (v_pk_maximum3_f16 on non-negative int16).
+template <int MODE, bool CIGAR, int NV, bool M3 = false>
 __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
-                                             uint32_t pass, bool last_pass, bool tdash, int lane) {
+                                             uint32_t pass, bool last_pass, bool tdash, int lane, int off = 0) {
     constexpr int R = kRows;
     constexpr bool LOCAL = MODE == kLocal;
+    static_assert(!M3 || LOCAL, "three-input maxima: local mode only");
+    if constexpr (!M3) off = 0;
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const int init = (MODE == kGlobal) ? gap : 0;
     const int zstep = 1 - 16 * ma;  // local: S(0, j) = zstep * j
@@ -65,10 +70,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     for (int r = 0; r < R; ++r) {
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
         q2[r] = i0 < n ? ((uint32_t)io.Q[0][i0] | ((uint32_t)io.Q[1][i0] << 16)) : 0u;
-        H2[r] = rep16(LOCAL ? -(int)(i0 + 1) : wmul(i0 + 1, init));  // S(i, 0)
+        H2[r] = rep16(LOCAL ? off - (int)(i0 + 1) : wmul(i0 + 1, init));  // S(i, 0)
     }
     const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
-    uint32_t recv = rep16(LOCAL ? -(int)ia : wmul(ia, init));
+    uint32_t recv = rep16(LOCAL ? off - (int)ia : wmul(ia, init));
     uint32_t tc2 = 0;
     const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
     // Per-lane running values, both pairs packed, advanced once per step:
@@ -77,7 +82,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // (all at t = -1 here).  Running bests are updated branch-free: the sign
     // of a saturating packed difference, spread over its half by v_perm,
     // selects the new column with one v_bfi; the value is a packed max.
-    uint32_t Zp = rep16(zstep * (0 - lane) - (int)(ia + 1));
+    uint32_t Zp = rep16(off + zstep * (0 - lane) - (int)(ia + 1));
     const uint32_t ZS2 = rep16(zstep);
     uint32_t jj = rep16(-lane), maj = rep16(-ma * lane);
     const uint32_t MA2 = rep16(ma);
@@ -119,7 +124,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         constexpr bool MASKED = decltype(masked_tag)::value;
         uint32_t top;
         if (pass == 0) {
-            top = rep16(LOCAL ? zstep * (int)(t + 1) : (init - ma) * (int)(t + 1));  // S(0, j)
+            top = rep16(LOCAL ? off + zstep * (int)(t + 1) : (init - ma) * (int)(t + 1));  // S(0, j)
         } else {
             top = (uint32_t)rdlane(bcur, t & 63u);
         }
@@ -157,8 +162,9 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
                 const uint32_t up = pk_add(upv, GUG);
                 const uint32_t m1 = pk_max(diag, left);
-                const uint32_t u = pk_max(m1, up);
-                const uint32_t hv = LOCAL ? pk_max(u, Z) : u;  // clamp, :185
+                uint32_t hv;
+                if constexpr (M3) hv = pk_max3_pos(m1, up, Z);  // clamp folded in, :185
+                else hv = LOCAL ? pk_max(pk_max(m1, up), Z) : pk_max(m1, up);
                 if (CIGAR) {
                     // raw compares (D wins over I in the walk; local walks track the
                     // cost instead of reading a STOP code, ta_device.h WalkSeq)
@@ -173,10 +179,17 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             });
             if (LOCAL) {
                 // balanced trees (a serial packed-max chain stalls one cycle per link)
-                const uint32_t lo = tree_max<0, NV>(H2);
+                uint32_t lo, hi_rows = 0;
+                if constexpr (M3) {
+                    lo = max3_reduce<NV>(H2);
+                    if constexpr (NV != R) hi_rows = max3_reduce<R - NV>(H2 + NV);
+                } else {
+                    lo = tree_max<0, NV>(H2);
+                    if constexpr (NV != R) hi_rows = tree_max<NV, R>(H2);
+                }
                 uint32_t sk = lo;
                 if (NV != R) {
-                    const uint32_t full = pk_max(lo, tree_max<NV, R>(H2));
+                    const uint32_t full = pk_max(lo, hi_rows);
                     sk = ((uint32_t)lane == nl - 1) ? lo : full;
                 }
                 // key = S - Zb = 16H - r per half; strict '>' keeps the first column (:186)
@@ -269,6 +282,20 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
                                                 uint32_t pass, bool last_pass, bool tdash, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
+    if constexpr (MODE == kLocal) {
+        const int off = local_max3_offset(n, m, a.match, a.mismatch, a.gap);  // wave-uniform
+        if (off >= 0) {
+            if (nv == kRows) return dual_pass<MODE, CIGAR, kRows, true>(a, io, n, m, pass, last_pass, tdash, lane, off);
+#define TA_NV_CASE(k) \
+    case k: return dual_pass<MODE, CIGAR, k, true>(a, io, n, m, pass, last_pass, tdash, lane, off);
+            switch (nv) {
+                TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
+                TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
+                default: TA_NV_CASE(15)
+            }
+#undef TA_NV_CASE
+        }
+    }
     if (MODE == kGlobal || nv == kRows) return dual_pass<MODE, CIGAR, kRows>(a, io, n, m, pass, last_pass, tdash, lane);
 #define TA_NV_CASE(k) \
     case k: return dual_pass<MODE, CIGAR, k>(a, io, n, m, pass, last_pass, tdash, lane);

@@ -116,22 +116,28 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     const uint32_t nlh[2] = {nl, (min((uint32_t)kPassRows, io.n[1] - row_base) + R - 1) / R};
     const bool has_next = !last_pass;
 
+    constexpr bool LOCAL = MODE == kLocal;
+    // local: every value is kept in [0, 0x7BFF] (flex_local_fits) so the clamp
+    // folds into a three-input max (pk_max3_pos): the offsets start the
+    // smallest clamp base of the wave at C0 and every rebase puts it back there
+    // -- a margin for 64 steps of drift and one step of candidates below it.
+    const int amag = max(max(abs(ma), abs(mi)), abs(gap));
+    const int C0 = LOCAL ? 64 * abs(ma) + 16 * amag + 64 : 0;
     // offsets: S(i, 0) = i * init, so start from the pass's first row
-    int O[2] = {wmul(row_base, init), wmul(row_base, init)};
+    int O[2] = {wmul(row_base, init) - C0, wmul(row_base, init) - C0};
     uint32_t q2[R], H2[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
         q2[r] = (i0 < io.n[0] ? (uint32_t)io.Q[0][i0] : 0u) | ((i0 < io.n[1] ? (uint32_t)io.Q[1][i0] : 0u) << 16);
-        H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init));  // S(i, 0) - O
+        H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init) + C0);  // S(i, 0) - O
     }
-    uint32_t recv = rep16(wmul((uint32_t)lane * R, init));
+    uint32_t recv = rep16(wmul((uint32_t)lane * R, init) + C0);
     uint32_t tc2 = 0;
     // local: clamp base Z = -ma*j - O per half (j = -lane before step 0), ma*j
     // (int32), the running best key 16*H + 15 - r and its column per pair
-    constexpr bool LOCAL = MODE == kLocal;
     const uint32_t MA2 = rep16(ma);
-    uint32_t Z = LOCAL ? rep16(ma * lane) : 0u;
+    uint32_t Z = LOCAL ? rep16(ma * lane + C0) : 0u;
     int mj = -ma * lane;
     int bestk[2] = {INT_MIN, INT_MIN};
     uint32_t bestj[2] = {0, 0};
@@ -167,8 +173,11 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         if (pass > 0) {
             load_rec_chunk(io, M, t >> 6, lane, bcur);
         }
-        // rebase (every 64 steps, all lanes alike): a lane that holds current cells
-        const uint32_t d = (uint32_t)rdlane((int)H2[0], t < M ? 0u : nl - 1);
+        // rebase (every 64 steps, all lanes alike): a lane that holds current cells;
+        // local: the wave's smallest clamp base (lane 0 when ma >= 0: Z falls with
+        // j) back to C0
+        const uint32_t d = LOCAL ? pk_sub((uint32_t)rdlane((int)Z, ma >= 0 ? 0u : 63u), rep16(C0))
+                                 : (uint32_t)rdlane((int)H2[0], t < M ? 0u : nl - 1);
 #pragma unroll
         for (int r = 0; r < R; ++r) H2[r] = pk_sub(H2[r], d);
         recv = pk_sub(recv, d);
@@ -240,8 +249,9 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
                 const uint32_t up = pk_add(upv, GUG);
                 const uint32_t m1 = pk_max(diag, left);
-                const uint32_t u = pk_max(m1, up);
-                const uint32_t hv = LOCAL ? pk_max(u, Z) : u;  // clamp, :185
+                uint32_t hv;
+                if constexpr (LOCAL) hv = pk_max3_pos(m1, up, Z);  // clamp folded in, :185
+                else hv = pk_max(m1, up);
                 if (CIGAR) {
                     // raw compares (D wins over I in the walk; local walks track the cost)
                     const uint32_t wd = pk_sub_sat(m1, up);
@@ -253,19 +263,22 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 upv = hv;
             });
             if (LOCAL) {
-                // the lane's best row of this column per pair: key 16*(V_r - V_0) + 15 - r
+                // the lane's best row of this column per pair: key 16*(V_r - V_0) + 15 - r,
+                // + kKeyOff so that the keys are non-negative for the three-input max tree
+                constexpr int kKeyOff = 4096;  // |16*(V_r - V_0)| <= 16*15*2*mag < 4096 (flex_fits)
                 uint32_t K[R];
-                K[0] = 0x000F000Fu;
+                K[0] = rep16(kKeyOff + 15);
 #pragma unroll
-                for (int r = 1; r < R; ++r) K[r] = pk_mad_i16(pk_sub(H2[r], H2[0]), 0x00100010u, rep16(15 - r));
-                const uint32_t lo = tree_max<0, NV>(K);
+                for (int r = 1; r < R; ++r)
+                    K[r] = pk_mad_i16(pk_sub(H2[r], H2[0]), 0x00100010u, rep16(kKeyOff + 15 - r));
+                const uint32_t lo = max3_reduce<NV>(K);
                 uint32_t kA = lo, kB = lo;
-                if (NV != R) {  // the pair's last lane holds NV valid rows
-                    const uint32_t full = pk_max(lo, tree_max<NV, R>(K));
+                if constexpr (NV != R) {  // the pair's last lane holds NV valid rows
+                    const uint32_t full = pk_max(lo, max3_reduce<R - NV>(K + NV));
                     kA = ((uint32_t)lane == nlh[0] - 1) ? lo : full;
                     kB = ((uint32_t)lane == nlh[1] - 1) ? lo : full;
                 }
-                const int kk[2] = {sext_lo(kA), sext_hi(kB)};
+                const int kk[2] = {sext_lo(kA) - kKeyOff, sext_hi(kB) - kKeyOff};
                 const int v0[2] = {sext_lo(H2[0]), sext_hi(H2[0])};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {

@@ -388,7 +388,10 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
 
 #ifdef TA_TU_MISC
 template <int MODE>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8))) void traceback_kernel(TraceArgs a) {
+#ifndef TA_TB_WPE
+#define TA_TB_WPE 8  // waves per SIMD the traceback kernel is compiled for
+#endif
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_TB_WPE))) void traceback_kernel(TraceArgs a) {
     // Wave-strided over the pairs (one wave per pair: the grid covers them all).
     const int lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * kWavesPerBlock;

@@ -24,6 +24,30 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 
 enum Mode : int { kGlobal = 0, kLocal = 1, kSemi = 2 };
 
+// Local dual fill (ta_dual.hip) with three-input maxima: its biased values
+// S = 16H + z*j - i (z = 1 - 16*ma) and every candidate, shifted by the
+// returned offset, lie in [0, 0x7BFF] -- non-negative int16 whose bit
+// patterns, read as f16, are finite and ordered like the integers, so
+// v_pk_maximum3_f16 takes their max.  Bounds: a local path into (i, j) has at
+// most min(i, j) diagonal steps and i + j gap steps, so
+//   H <= hs*j + gp*(i + j)   (hs = max(0, ma, mi), gp = max(0, gap))
+//   S <= (16hs + 16gp + z)*j + (16gp - 1)*i,   S >= z*j - i (the clamp),
+// rows up to n + 15 (the last lane's padding rows), candidates one step
+// (<= 16*mag) below the clamp.  -1: does not fit (the max/max kernel runs).
+TA_HD inline int local_max3_offset(uint32_t n, uint32_t m, int ma, int mi, int gap) {
+    const long long N = (long long)n + 16, M = m;
+    const long long ama = ma < 0 ? -ma : ma, ami = mi < 0 ? -mi : mi, ag = gap < 0 ? -gap : gap;
+    const long long mag = ama > ami ? (ama > ag ? ama : ag) : (ami > ag ? ami : ag);
+    const long long hs = ma > mi ? (ma > 0 ? ma : 0) : (mi > 0 ? mi : 0);
+    const long long gp = gap > 0 ? gap : 0;
+    const long long z = 1 - 16LL * ma;
+    const long long cj = 16 * hs + 16 * gp + z, ci = 16 * gp - 1;
+    const long long hi = (cj > 0 ? cj * M : 0) + (ci > 0 ? ci * N : 0) + 32 * (mag + 1);
+    const long long lo = (z < 0 ? z * M : 0) - N - 32 * (mag + 1);
+    if (hi - lo > 0x7BFF) return -1;
+    return (int)(-lo);
+}
+
 // Steps of one pass over an m-column target: m + 63 (lane skew).
 TA_HD inline uint32_t pass_steps(uint32_t m) { return m + kWave - 1; }
 TA_HD inline uint32_t n_passes(uint32_t n) { return (n + kPassRows - 1) / kPassRows; }

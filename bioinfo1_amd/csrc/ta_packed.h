@@ -27,6 +27,33 @@ __device__ __forceinline__ uint32_t tree_max(const uint32_t* v) {
     if constexpr (E - B == 1) return v[B];
     else return pk_max(tree_max<B, (B + E) / 2>(v), tree_max<(B + E) / 2, E>(v));
 }
+// max of three packed values whose halves all lie in [0, 0x7BFF]: read as
+// f16 bit patterns they are finite non-negative numbers ordered like the
+// integers, and clang fuses the nested maxima into one v_pk_maximum3_f16
+// (gfx950; there is no packed i16 max3).  The result is one of the inputs'
+// bit patterns.
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint32_t pk_max3_pos(uint32_t a, uint32_t b, uint32_t c) {
+    const h2v x = __builtin_bit_cast(h2v, a), y = __builtin_bit_cast(h2v, b), z = __builtin_bit_cast(h2v, c);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
+}
+// max over v[0..N) of such values: triples per level, ceil((N-1)/2) instructions
+template <int N>
+__device__ __forceinline__ uint32_t max3_reduce(const uint32_t* v) {
+    if constexpr (N == 1) {
+        return v[0];
+    } else if constexpr (N == 2) {
+        return pk_max(v[0], v[1]);
+    } else {
+        constexpr int M = (N + 2) / 3;
+        uint32_t w[M];
+#pragma unroll
+        for (int k = 0; k < N / 3; ++k) w[k] = pk_max3_pos(v[3 * k], v[3 * k + 1], v[3 * k + 2]);
+        if constexpr (N % 3 == 1) w[M - 1] = v[N - 1];
+        if constexpr (N % 3 == 2) w[M - 1] = pk_max(v[N - 2], v[N - 1]);
+        return max3_reduce<M>(w);
+    }
+}
 // Packed helpers through clang vector builtins (inline asm costs an s_nop:
 // the hazard recognizer cannot see into it).  pk_min_u16 must get a
 // non-constant operand: min(x, 1) with a literal 1 is expanded into compares.
