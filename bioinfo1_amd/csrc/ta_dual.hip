@@ -43,7 +43,9 @@ struct DualIo {
 // M3 (local only): every value carries the offset `off` (local_max3_offset)
 // so that the clamp folds into a three-input max and the stripe's row max is
 // a tree of three-input maxima (v_pk_maximum3_f16 on non-negative int16).
-template <int MODE, bool CIGAR, int NV, bool M3 = false>
+// CLS: both queries hold only A, C, G, T -- mismatch flags by table lookup
+// (ta_packed.h mismatch_table / row_selector), one v_perm per row.
+template <int MODE, bool CIGAR, int NV, bool M3, bool CLS>
 __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
                                              uint32_t pass, bool last_pass, bool tdash, int lane, int off = 0) {
     constexpr int R = kRows;
@@ -69,12 +71,13 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
-        q2[r] = i0 < n ? ((uint32_t)io.Q[0][i0] | ((uint32_t)io.Q[1][i0] << 16)) : 0u;
+        if constexpr (CLS) q2[r] = i0 < n ? row_selector(io.Q[0][i0], io.Q[1][i0]) : row_selector(0, 0);
+        else q2[r] = i0 < n ? ((uint32_t)io.Q[0][i0] | ((uint32_t)io.Q[1][i0] << 16)) : 0u;
         H2[r] = rep16(LOCAL ? off - (int)(i0 + 1) : wmul(i0 + 1, init));  // S(i, 0)
     }
     const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
     uint32_t recv = rep16(LOCAL ? off - (int)ia : wmul(ia, init));
-    uint32_t tc2 = 0;
+    uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
     const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
     // Per-lane running values, both pairs packed, advanced once per step:
     //   Zp = local clamp base Zb = zstep*j - (ia + 1) for this lane's column j
@@ -134,7 +137,13 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
         const uint32_t prev = recv;
         recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
-        tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        if constexpr (CLS) {
+            tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
+            tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
+            if (tdash) tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        } else {
+            tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        }
         Zp = pk_add(Zp, ZS2);
         jj = pk_add(jj, ONE);
         if (MODE == kSemi) maj = pk_add(maj, MA2);
@@ -150,7 +159,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 const int gb = ((tc2 >> 16) == '-') ? gld : glg;
                 GL = ((uint32_t)ga & 0xFFFFu) | ((uint32_t)gb << 16);
             }
-            auto e_of = [&](int r) { return pk_min_u16(q2[r] ^ tc2, ONE); };  // 0 on a match, 1 otherwise
+            auto e_of = [&](int r) {  // 0 on a match, 1 otherwise
+                if constexpr (CLS) return mismatch_flags(tA, tB, q2[r]);
+                else return pk_min_u16(q2[r] ^ tc2, ONE);
+            };
             uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
             uint32_t upv = recv;
             uint32_t Z = Zp;
@@ -277,7 +289,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     return out;
 }
 
-template <int MODE, bool CIGAR>
+template <int MODE, bool CIGAR, bool CLS>
 __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
                                                 uint32_t pass, bool last_pass, bool tdash, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
@@ -285,9 +297,10 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
     if constexpr (MODE == kLocal) {
         const int off = local_max3_offset(n, m, a.match, a.mismatch, a.gap);  // wave-uniform
         if (off >= 0) {
-            if (nv == kRows) return dual_pass<MODE, CIGAR, kRows, true>(a, io, n, m, pass, last_pass, tdash, lane, off);
+            if (nv == kRows)
+                return dual_pass<MODE, CIGAR, kRows, true, CLS>(a, io, n, m, pass, last_pass, tdash, lane, off);
 #define TA_NV_CASE(k) \
-    case k: return dual_pass<MODE, CIGAR, k, true>(a, io, n, m, pass, last_pass, tdash, lane, off);
+    case k: return dual_pass<MODE, CIGAR, k, true, CLS>(a, io, n, m, pass, last_pass, tdash, lane, off);
             switch (nv) {
                 TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
                 TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -296,9 +309,10 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
 #undef TA_NV_CASE
         }
     }
-    if (MODE == kGlobal || nv == kRows) return dual_pass<MODE, CIGAR, kRows>(a, io, n, m, pass, last_pass, tdash, lane);
+    if (MODE == kGlobal || nv == kRows)
+        return dual_pass<MODE, CIGAR, kRows, false, CLS>(a, io, n, m, pass, last_pass, tdash, lane);
 #define TA_NV_CASE(k) \
-    case k: return dual_pass<MODE, CIGAR, k>(a, io, n, m, pass, last_pass, tdash, lane);
+    case k: return dual_pass<MODE, CIGAR, k, false, CLS>(a, io, n, m, pass, last_pass, tdash, lane);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -324,15 +338,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     p[1] = a.order[2 * (a.begin + widx) + 1];
     const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
     DualIo io;
-    bool tdash = false, qdash = false;
+    bool tdash = false, qdash = false, qother = false;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         io.Q[h] = a.qbytes + a.qoff[p[h]];
         io.T[h] = a.tbytes + a.toff[p[h]];
         io.ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
         for (uint32_t k = (uint32_t)lane; k < m; k += 64) tdash |= io.T[h][k] == '-';
-        for (uint32_t k = (uint32_t)lane; k < n; k += 64) qdash |= io.Q[h][k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < n; k += 64) {
+            const uint32_t c = io.Q[h][k];
+            qdash |= c == '-';
+            qother |= !is_acgt(c);
+        }
     }
+    const bool cls = __ballot(qother) == 0;  // queries of A, C, G, T only: table mismatch flags
     // A '-' in a query changes the up gain per row; that variant would cost
     // this kernel ~30 VGPRs for input real reads never contain, so such
     // couples go to the int32 fill (launched right after, same workspace).
@@ -357,7 +376,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     }
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const bool last_pass = pass + 1 == passes;
-        const DualOut o = dual_pass_nv<MODE, CIGAR>(a, io, n, m, pass, last_pass, tdash, lane);
+        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, pass, last_pass, tdash, lane)
+                              : dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, pass, last_pass, tdash, lane);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (MODE != kGlobal && o.o[h].h > best_h[h]) {

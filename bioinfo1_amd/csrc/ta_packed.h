@@ -54,6 +54,27 @@ __device__ __forceinline__ uint32_t max3_reduce(const uint32_t* v) {
         return max3_reduce<M>(w);
     }
 }
+// Mismatch flags from a per-step table, for queries of the bytes A, C, G, T
+// only (the reference compares raw bytes; any other target byte can then
+// match no query byte).  class: 'A' 0, 'C' 1, 'T' 2, 'G' 3 = (c >> 1) & 3.
+// The table of target byte c has byte k = 0 if c is the class-k letter,
+// else 1; row r's selector picks pair A's flag from table A (bytes 0-3),
+// pair B's from table B (4-7) and zeros above them: one v_perm_b32 per row
+// instead of xor + min.  The tables are built on the SALU from the
+// wave-uniform new target byte and ride the lane skew with DPP.
+__device__ __forceinline__ bool is_acgt(uint32_t c) {
+    return c == ((0x47544341u >> (8u * ((c >> 1) & 3u))) & 0xFFu);
+}
+__device__ __forceinline__ uint32_t mismatch_table(uint32_t c) {
+    const uint32_t sh = 8u * ((c >> 1) & 3u);
+    return 0x01010101u ^ ((uint32_t)(c == ((0x47544341u >> sh) & 0xFFu)) << sh);
+}
+__device__ __forceinline__ uint32_t row_selector(uint32_t qa, uint32_t qb) {
+    return ((qa >> 1) & 3u) | 0x0C00u | ((4u + ((qb >> 1) & 3u)) << 16) | 0x0C000000u;
+}
+__device__ __forceinline__ uint32_t mismatch_flags(uint32_t ta, uint32_t tb, uint32_t sel) {
+    return __builtin_amdgcn_perm(tb, ta, sel);
+}
 // Packed helpers through clang vector builtins (inline asm costs an s_nop:
 // the hazard recognizer cannot see into it).  pk_min_u16 must get a
 // non-constant operand: min(x, 1) with a literal 1 is expanded into compares.
