@@ -263,7 +263,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         t.match = h.match;
         t.mismatch = h.mismatch;
         t.gap = h.gap;
-        TA_HIP(ctx, ta::launch_traceback(h.type, t, s));
+        TA_HIP(ctx, ta::launch_traceback(h.type, t, s, h.walk_group));
         roctxRangePop();
     }
     return TA_OK;

@@ -95,7 +95,8 @@ struct CompactArgs {
 hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_fill_mode(bool wide, const FillArgs& a, hipStream_t s);
-hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s);
+// group: 32 = local walks of two pairs per wave (ta_walk2.h), 0 = one pair per wave
+hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int group);
 // Dual-pair packed int16 fill (ta_dual.hip): a.order holds 2 pair ids per wave.
 hipError_t launch_dual(int mode, bool cigar, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>

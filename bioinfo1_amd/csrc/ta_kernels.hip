@@ -27,6 +27,7 @@
 #include <cstdlib>
 
 #include "ta_device.h"
+#include "ta_walk2.h"
 
 namespace ta {
 namespace {
@@ -411,6 +412,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_TB_WP
     }
 }
 
+// Local walks, 64/G pairs per wave (ta_walk2.h).
+template <int G>
+__global__ __launch_bounds__(kBlock) void traceback_group_kernel(TraceArgs a) {
+    const uint32_t widx = wave_id();
+    if ((64u / G) * widx >= a.count) return;
+    traceback_group_local<G>(a, widx, threadIdx.x & 63);
+}
+
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t p = wave_id();
@@ -482,9 +491,13 @@ hipError_t launch_flex(int mode, bool cigar, const FillArgs& a, hipStream_t s) {
     }
 }
 
-hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s) {
+hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int group) {
     if (!a.count) return hipSuccess;
     const dim3 g = grid_for(a.count), b(kBlock);
+    if (mode == kLocal && group == 32) {
+        hipLaunchKernelGGL(traceback_group_kernel<32>, grid_for((a.count + 1) / 2), b, 0, s, a);
+        return hipGetLastError();
+    }
     switch (mode) {
         case kGlobal: hipLaunchKernelGGL(traceback_kernel<kGlobal>, g, b, 0, s, a); break;
         case kLocal: hipLaunchKernelGGL(traceback_kernel<kLocal>, g, b, 0, s, a); break;

@@ -293,6 +293,14 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     // A fill kernel that walks its own pair only pays when nothing else of the
     // chunk runs in the separate traceback kernel anyway.
     pl.fused = want_cigar && pl.n_dual_pairs == 0 && !(flags & kPlanUnfused);
+    // Local walks, two pairs per wave (32 lanes each, ta_walk2.h): 0.65 vs 0.77 ms on
+    // config 2 (16 lanes each: 0.75, too few waves to hide latency).  Their runs are
+    // clipped to 32 cells, so batches of long pairs (long M runs) keep the one-pair
+    // walk (config 3 local: 4.1 vs 6.3 ms).  24-bit multiplies of the scores.
+    uint64_t len_sum = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) len_sum += (uint64_t)qlen[p] + tlen[p];
+    const bool short_pairs = len_sum <= 6000ull * std::max<uint32_t>(n_pairs, 1);
+    pl.walk_group = ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) ? 0 : 32;
     pl.flex_task_off.assign(1, 0);
     for (size_t w = 0; w < pl.flexes.size() / 2; ++w)
         pl.flex_task_off.push_back(pl.flex_task_off.back() + n_passes(qlen[pl.flexes[2 * w]]));

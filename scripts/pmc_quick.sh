@@ -19,7 +19,13 @@ for row in csv.DictReader(open(f[0])):
     acc[row["Kernel_Name"]][row["Counter_Name"]].append(float(row["Counter_Value"]))
 bl = [json.loads(l) for l in open(out + "/pmc.log") if l.startswith("{")][-1]
 cells = bl["config"]["cells_per_gpu"]; ch = bl.get("chunks", 1)
+pairs = bl["config"]["pairs_per_gpu"]
 for k, cs in acc.items():
+    if "traceback" in k:
+        v = sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"])
+        s = sum(cs["SQ_INSTS_SALU"]) / len(cs["SQ_INSTS_SALU"])
+        l = sum(cs["SQ_INSTS_LDS"]) / len(cs["SQ_INSTS_LDS"])
+        print(k[:70], "per pair: VALU %.0f SALU %.0f LDS %.0f" % (v * ch / pairs, s * ch / pairs, l * ch / pairs))
     if "fill" in k:
         v = sum(cs["SQ_INSTS_VALU"]) / len(cs["SQ_INSTS_VALU"])
         s = sum(cs["SQ_INSTS_SALU"]) / len(cs["SQ_INSTS_SALU"])

@@ -9,7 +9,8 @@ import pytest
 from conftest import DIGESTS, ROOT, cigar_digest, digest_batch, load_digest, run_plan
 
 from bioinfo1_amd import synth
-from bioinfo1_amd.align import TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, Aligner, DevicePlan, align
+from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, Aligner, DevicePlan,
+                                align)
 from oracle.pyoracle import Oracle
 
 pytestmark = pytest.mark.gpu
@@ -143,7 +144,7 @@ def test_dual_fuzz(aligner, oracle, case):
     plan.close()
     want = oracle.align_batch(b, mode, *sc, True)
     # packed kernels (default), the int32 kernel alone (fused / separate walk)
-    for flags in (0, TA_PLAN_INT32_ONLY, TA_PLAN_INT32_ONLY | TA_PLAN_UNFUSED):
+    for flags in (0, TA_PLAN_WALK1, TA_PLAN_INT32_ONLY, TA_PLAN_INT32_ONLY | TA_PLAN_UNFUSED):
         for cig in (True, False):
             got = run_plan(aligner, b, mode, sc, cig, flags)
             np.testing.assert_array_equal(got.scores, want.scores)
