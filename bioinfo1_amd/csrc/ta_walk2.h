@@ -159,25 +159,28 @@ __device__ __forceinline__ void traceback_group_local(const TraceArgs& a, uint32
         const uint32_t hrun = min(streak, iflag ? j : min(j, r + 1u));
         const uint32_t run = live ? (dflag ? drun : hrun) : 0u;
         const uint32_t op = live ? (dflag ? 'D' : ('M' - 4u * iflag)) : w.op;
-        // the bytes of the run's cells (lane li: q[i-1-li], t[j-1-li]) from 64-byte
-        // windows refilled after G rows / columns of progress
-        if (live && qbase - i > (uint32_t)G) {
-            qbase = i;
-            qw = seq_window_g<G>(Q, i, li);
-        }
-        if (live && tbase - j > (uint32_t)G) {
-            tbase = j;
-            tw = seq_window_g<G>(T, j, li);
-        }
-        const uint32_t oq = qbase - i + li, ot = tbase - j + li;  // < 2G
-        const uint32_t qb = (gread<G>(qw, h, oq) >> ((oq / G) << 3)) & 0xFFu;
-        const uint32_t tb = (gread<G>(tw, h, ot) >> ((ot / G) << 3)) & 0xFFu;
         // cost along the run (traceback_pair: move k leaves cell c_k; the walk stops
         // at the first c_k whose cost is 0)
         const bool gfast = op != 'M' && (op == 'D' ? gfastD : gfastI);
         const uint32_t inrun = run >= 32u ? ~0u : ((1u << run) - 1u);
-        const int c = __builtin_popcount(group_bits<G>(ballot(qb == tb), h) & inrun);  // matches of an M run
-        // (24-bit multiplies: run, c <= 32 and |scores| < 2^22, checked by the planner)
+        uint32_t qb = 0, tb = 0;
+        int c = 0;
+        if (ballot(live && !gfast)) {
+            // the bytes of the run's cells (lane li: q[i-1-li], t[j-1-li]) from 2G-byte
+            // windows refilled after G rows / columns of progress
+            if (live && qbase - i > (uint32_t)G) {
+                qbase = i;
+                qw = seq_window_g<G>(Q, i, li);
+            }
+            if (live && tbase - j > (uint32_t)G) {
+                tbase = j;
+                tw = seq_window_g<G>(T, j, li);
+            }
+            const uint32_t oq = qbase - i + li, ot = tbase - j + li;  // < 2G
+            qb = (gread<G>(qw, h, oq) >> ((oq / G) << 3)) & 0xFFu;
+            tb = (gread<G>(tw, h, ot) >> ((ot / G) << 3)) & 0xFFu;
+            c = __builtin_popcount(group_bits<G>(ballot(qb == tb), h) & inrun);  // matches of an M run
+        }
         const bool whole = gfast || (op == 'M' && H > __mul24((int)run, posM));  // the run cannot reach cost 0
         int Hn = gfast ? H - __mul24((int)run, gap) : H - (__mul24((int)run, mi) + __mul24(c, ma - mi));
         uint32_t emit = run;
