@@ -90,24 +90,33 @@ struct GroupWriter {
     }
 };
 
-// Local walks of pairs k = (64/G)*widx + h of the launch (a.order).
+// One group's pair (has = false: the group idles through the walk).
+struct GroupPair {
+    bool has;
+    uint32_t n, m, gi, gj;
+    int score;
+    const uint32_t* P;  // the pair's codes
+    const uint8_t* Q;
+    const uint8_t* T;
+    char* slot;  // the pair's CIGAR slot (cigar_slot_bytes(n, m))
+};
+
+// The local walk of group lane / G's pair; returns the CIGAR's start in the
+// slot and its length (the same in every lane of the group).
 template <int G>
-__device__ __forceinline__ void traceback_group_local(const TraceArgs& a, uint32_t widx, int lane) {
-    constexpr uint32_t NG = 64 / G;
+__device__ __forceinline__ void walk_group_local(const GroupPair& gp, int ma, int mi, int gap, int lane,
+                                                 uint64_t* start_in_slot, uint32_t* len) {
     const uint32_t h = (uint32_t)lane / G, li = (uint32_t)lane % G;
-    const uint32_t k = NG * widx + h;
-    const bool has = k < a.count;
-    const uint32_t p = has ? (a.order ? a.order[a.begin + k] : a.begin + k) : 0u;
-    const uint32_t n = has ? a.qlen[p] : 0u, m = has ? a.tlen[p] : 0u;
-    const uint32_t* P = a.ptrs + (has ? a.ptr_off[p] : 0ull);
-    const uint8_t* Q = a.qbytes + (has ? a.qoff[p] : 0ull);
-    const uint8_t* T = a.tbytes + (has ? a.toff[p] : 0ull);
+    const bool has = gp.has;
+    const uint32_t n = gp.n, m = gp.m;
+    const uint32_t* P = gp.P;
+    const uint8_t* Q = gp.Q;
+    const uint8_t* T = gp.T;
     const uint64_t cap = cigar_slot_bytes(n, m);
-    const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const int posM = max(0, max(ma, mi));
-    GroupWriter<G> w{a.slots + (has ? a.slot_off[p] : 0ull) + cap, 0u, 0u, 0u, 0u, 0u, 0u, h, li};
-    uint32_t i = has ? a.goal_i[p] : 0u, j = has ? a.goal_j[p] : 0u;
-    int H = has ? a.score[p] : 0;
+    GroupWriter<G> w{gp.slot + cap, 0u, 0u, 0u, 0u, 0u, 0u, h, li};
+    uint32_t i = gp.gi, j = gp.gj;
+    int H = gp.score;
     // gap runs need no bytes when their sequence has no '-' and gap <= 0
     bool qd = false, td = false;
     for (uint32_t x = li; x < max(n, m); x += G) {
@@ -226,9 +235,40 @@ __device__ __forceinline__ void traceback_group_local(const TraceArgs& a, uint32
     const bool more = has && w.op;
     if (more) w.park();
     if (more && w.nb) w.flush();
-    if (has && li == 0) {
-        a.cigar_start[p] = a.slot_off[p] + (cap - w.used);
-        a.cigar_len[p] = w.used;
+    *start_in_slot = cap - w.used;
+    *len = w.used;
+}
+
+// Local walks of pairs k = (64/G)*widx + h of a traceback launch (a.order).
+template <int G>
+__device__ __forceinline__ void traceback_group_local(const TraceArgs& a, uint32_t widx, int lane) {
+    const uint32_t h = (uint32_t)lane / G, li = (uint32_t)lane % G;
+    const uint32_t k = (64u / G) * widx + h;
+    GroupPair gp{};
+    gp.has = k < a.count;
+    const uint32_t p = gp.has ? (a.order ? a.order[a.begin + k] : a.begin + k) : 0u;
+    if (gp.has) {
+        gp.n = a.qlen[p];
+        gp.m = a.tlen[p];
+        gp.gi = a.goal_i[p];
+        gp.gj = a.goal_j[p];
+        gp.score = a.score[p];
+        gp.P = a.ptrs + a.ptr_off[p];
+        gp.Q = a.qbytes + a.qoff[p];
+        gp.T = a.tbytes + a.toff[p];
+        gp.slot = a.slots + a.slot_off[p];
+    } else {
+        gp.P = a.ptrs;
+        gp.Q = a.qbytes;
+        gp.T = a.tbytes;
+        gp.slot = a.slots;
+    }
+    uint64_t st;
+    uint32_t len;
+    walk_group_local<G>(gp, a.match, a.mismatch, a.gap, lane, &st, &len);
+    if (gp.has && li == 0) {
+        a.cigar_start[p] = a.slot_off[p] + st;
+        a.cigar_len[p] = len;
     }
 }
 

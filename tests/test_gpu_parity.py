@@ -377,6 +377,32 @@ def test_local_walk_cost_tracking(aligner, oracle, sc):
         assert got.cigar(p) == want.cigar(p), (sc, p)
 
 
+@pytest.mark.parametrize("sc", [(1, -1, -1), (2, -3, -1), (1, -2, -3)])
+def test_local_group_walk_dual_and_fallback(aligner, oracle, sc):
+    """Local plans of equal-shape couples only, walked two pairs per wave
+    (ta_walk2.h); couples with a '-' query go to the int32 fill.  Against the
+    oracle, with the one-pair walk too."""
+    rng = np.random.default_rng(0xF05E + sc[0])
+    al, ald = np.frombuffer(b"ACGT", np.uint8), np.frombuffer(b"ACGT-N", np.uint8)
+    pairs = []
+    for k in range(96):
+        n, m = [(200, 180), (700, 650), (33, 900)][k % 3]
+        qa = ald if k % 17 == 0 else al
+        ta = ald if k % 5 == 0 else al
+        pairs.append((qa[rng.integers(len(qa), size=n)].tobytes(), ta[rng.integers(len(ta), size=m)].tobytes()))
+    b = synth.from_pairs(pairs)
+    plan = DevicePlan(aligner, b, 1, *sc, True)
+    assert plan.dual_pairs == 96 and not plan.fused, (plan.dual_pairs, plan.fused)
+    plan.close()
+    want = oracle.align_batch(b, 1, *sc, True)
+    for flags in (0, TA_PLAN_WALK1):
+        got = run_plan(aligner, b, 1, sc, True, flags)
+        np.testing.assert_array_equal(got.scores, want.scores)
+        np.testing.assert_array_equal(got.target_begins, want.target_begins)
+        for p in range(b.n_pairs):
+            assert got.cigar(p) == want.cigar(p), (sc, flags, p)
+
+
 def test_config5_shape_multichunk(aligner):
     """Config 5 shape forced through >= 4 chunks (small workspace budget):
     every chunk reuses the code workspace; the first 32 pairs bit-exact vs the
