@@ -66,8 +66,10 @@ __device__ __forceinline__ bool is_acgt(uint32_t c) {
     return c == ((0x47544341u >> (8u * ((c >> 1) & 3u))) & 0xFFu);
 }
 __device__ __forceinline__ uint32_t mismatch_table(uint32_t c) {
+    // (a select of the bit, not a bool shifted: keeps the whole table on the SALU)
     const uint32_t sh = 8u * ((c >> 1) & 3u);
-    return 0x01010101u ^ ((uint32_t)(c == ((0x47544341u >> sh) & 0xFFu)) << sh);
+    const uint32_t bit = 1u << sh;
+    return 0x01010101u ^ ((c == ((0x47544341u >> sh) & 0xFFu)) ? bit : 0u);
 }
 __device__ __forceinline__ uint32_t row_selector(uint32_t qa, uint32_t qb) {
     return ((qa >> 1) & 3u) | 0x0C00u | ((4u + ((qb >> 1) & 3u)) << 16) | 0x0C000000u;
