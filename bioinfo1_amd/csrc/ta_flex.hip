@@ -96,7 +96,9 @@ __device__ __forceinline__ void load_rec_chunk(const FlexIo& io, uint32_t M, uin
     }
 }
 
-template <int MODE, bool CIGAR, int NV>
+// CLS: both queries hold only A, C, G, T -- mismatch flags by table lookup
+// (ta_packed.h mismatch_table / row_selector), one v_perm per row.
+template <int MODE, bool CIGAR, int NV, bool CLS>
 __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io, uint32_t pass, bool last_pass,
                                              bool tdash, int lane) {
     constexpr int R = kRows;
@@ -129,11 +131,12 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
-        q2[r] = (i0 < io.n[0] ? (uint32_t)io.Q[0][i0] : 0u) | ((i0 < io.n[1] ? (uint32_t)io.Q[1][i0] : 0u) << 16);
+        const uint32_t qa = i0 < io.n[0] ? (uint32_t)io.Q[0][i0] : 0u, qb = i0 < io.n[1] ? (uint32_t)io.Q[1][i0] : 0u;
+        q2[r] = CLS ? row_selector(qa, qb) : (qa | (qb << 16));
         H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init) + C0);  // S(i, 0) - O
     }
     uint32_t recv = rep16(wmul((uint32_t)lane * R, init) + C0);
-    uint32_t tc2 = 0;
+    uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
     // local: clamp base Z = -ma*j - O per half (j = -lane before step 0), ma*j
     // (int32), the running best key 16*H + 15 - r and its column per pair
     const uint32_t MA2 = rep16(ma);
@@ -222,7 +225,13 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
         const uint32_t prev = recv;
         recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
-        tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        if constexpr (CLS) {
+            tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
+            tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
+            if (tdash) tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        } else {
+            tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        }
         if (LOCAL) {
             Z = pk_sub(Z, MA2);
             mj += ma;
@@ -238,7 +247,10 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 const int gb = ((tc2 >> 16) == '-') ? gld : glg;
                 GL = ((uint32_t)ga & 0xFFFFu) | ((uint32_t)gb << 16);
             }
-            auto e_of = [&](int r) { return pk_min_u16(q2[r] ^ tc2, ONE); };
+            auto e_of = [&](int r) {  // 0 on a match, 1 otherwise
+                if constexpr (CLS) return mismatch_flags(tA, tB, q2[r]);
+                else return pk_min_u16(q2[r] ^ tc2, ONE);
+            };
             uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
             uint32_t upv = recv;
             static_for<0, R>([&](auto rc) {
@@ -368,14 +380,14 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     return out;
 }
 
-template <int MODE, bool CIGAR>
+template <int MODE, bool CIGAR, bool CLS>
 __device__ __forceinline__ FlexOut flex_pass_nv(const FillArgs& a, const FlexIo& io, uint32_t pass, bool last_pass,
                                                 bool tdash, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, io.n[0] - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
-    if (nv == kRows) return flex_pass<MODE, CIGAR, kRows>(a, io, pass, last_pass, tdash, lane);
+    if (nv == kRows) return flex_pass<MODE, CIGAR, kRows, CLS>(a, io, pass, last_pass, tdash, lane);
 #define TA_NV_CASE(k) \
-    case k: return flex_pass<MODE, CIGAR, k>(a, io, pass, last_pass, tdash, lane);
+    case k: return flex_pass<MODE, CIGAR, k, CLS>(a, io, pass, last_pass, tdash, lane);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -411,7 +423,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
     p[0] = a.order[2 * w];
     p[1] = a.order[2 * w + 1];
     FlexIo io;
-    bool tdash = false, qdash = false;
+    bool tdash = false, qdash = false, qother = false;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         io.n[h] = a.qlen[p[h]];
@@ -420,7 +432,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
         io.T[h] = a.tbytes + a.toff[p[h]];
         io.ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
         for (uint32_t k = (uint32_t)lane; k < io.m[h]; k += 64) tdash |= io.T[h][k] == '-';
-        for (uint32_t k = (uint32_t)lane; k < io.n[h]; k += 64) qdash |= io.Q[h][k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < io.n[h]; k += 64) {
+            const uint32_t c = io.Q[h][k];
+            qdash |= c == '-';
+            qother |= !is_acgt(c);
+        }
     }
     PassOut* po = static_cast<PassOut*>(a.pout) + 2ull * g;
     if (__ballot(qdash)) {  // per-row up gains: the int32 fill takes the couple (pass 0's wave hands it over)
@@ -449,7 +465,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
     io.tag_w = a.epoch * 64u + pass + 1u;
     io.tag_r = a.epoch * 64u + pass;
     io.err = a.err;
-    const FlexOut o = flex_pass_nv<MODE, CIGAR>(a, io, pass, last_pass, tdash, lane);
+    const FlexOut o = __ballot(qother) == 0 ? flex_pass_nv<MODE, CIGAR, true>(a, io, pass, last_pass, tdash, lane)
+                                            : flex_pass_nv<MODE, CIGAR, false>(a, io, pass, last_pass, tdash, lane);
     if (lane == 0) {
         po[0] = o.o[0];
         po[1] = o.o[1];
