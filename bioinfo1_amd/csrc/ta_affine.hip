@@ -485,7 +485,9 @@ __global__ __launch_bounds__(kBlock) void affine_traceback_kernel(AffArgs a) {
 // The host sends only couples whose every value provably fits int16
 // (affine_fits_int16); a couple with '-' in a query goes back to the int32
 // fill through fb_list.
-template <int MODE, bool CIGAR, int NV>
+// CLS: both queries hold only A, C, G, T -- mismatch flags by table lookup
+// (ta_packed.h mismatch_table / row_selector), one v_perm per row.
+template <int MODE, bool CIGAR, int NV, bool CLS>
 __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* const (&Q)[2], const uint8_t* const (&T)[2],
                                               uint2* const (&ptrs)[2], uint2* B, uint32_t n, uint32_t m, uint32_t pass,
                                               bool last_pass, bool tdash, int lane, PassOut (&out)[2]) {
@@ -508,7 +510,8 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;  // row i0 + 1
-        q2[r] = i0 < n ? ((uint32_t)Q[0][i0] | ((uint32_t)Q[1][i0] << 16)) : 0u;
+        if constexpr (CLS) q2[r] = i0 < n ? row_selector(Q[0][i0], Q[1][i0]) : row_selector(0, 0);
+        else q2[r] = i0 < n ? ((uint32_t)Q[0][i0] | ((uint32_t)Q[1][i0] << 16)) : 0u;
         const int h0 = (MODE == kGlobal) ? O + (int)(i0 + 1) * X : 0;  // H(i, 0)
         H2[r] = rep16(h0);
         E2[r] = rep16(h0 - K);
@@ -516,7 +519,7 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
     const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
     uint32_t recvH = rep16((MODE == kGlobal && ia) ? O + (int)ia * X : 0);  // H(ia, 0)
     uint32_t recvF = 0, Flast = 0;
-    uint32_t tc2 = 0;
+    uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
     uint32_t maj = rep16(-ma * lane);  // ma*j at t = -1 (semi: row n holds H = S + ma*j)
     const uint32_t MA2 = rep16(ma);
     uint32_t jj = rep16(-lane);
@@ -573,7 +576,13 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
         const uint32_t prev = recvH;
         recvH = (uint32_t)wave_shr1((int)topH, (int)H2[R - 1]);
         recvF = (uint32_t)wave_shr1((int)topF, (int)Flast);
-        tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        if constexpr (CLS) {
+            tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
+            tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
+            if (tdash) tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        } else {
+            tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+        }
         jj = pk_add(jj, ONE);
         if (MODE == kSemi) maj = pk_add(maj, MA2);
 
@@ -587,7 +596,10 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
                 GOT = ((uint32_t)(da ? -ma : OX - ma) & 0xFFFFu) | ((uint32_t)(db ? -ma : OX - ma) << 16);
                 GET = ((uint32_t)(da ? -ma : X - ma) & 0xFFFFu) | ((uint32_t)(db ? -ma : X - ma) << 16);
             }
-            auto e_of = [&](int r) { return pk_min_u16(q2[r] ^ tc2, ONE); };
+            auto e_of = [&](int r) {  // 0 on a match, 1 otherwise
+                if constexpr (CLS) return mismatch_flags(tA, tB, q2[r]);
+                else return pk_min_u16(q2[r] ^ tc2, ONE);
+            };
             uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
             uint32_t upH = recvH, upF = recvF;
             static_for<0, R>([&](auto rc) {
@@ -684,7 +696,7 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
     }
 }
 
-template <int MODE, bool CIGAR>
+template <int MODE, bool CIGAR, bool CLS>
 __device__ __forceinline__ void aff_dual_pass_nv(const AffArgs& a, const uint8_t* const (&Q)[2],
                                                  const uint8_t* const (&T)[2], uint2* const (&ptrs)[2], uint2* B,
                                                  uint32_t n, uint32_t m, uint32_t pass, bool last_pass, bool tdash,
@@ -692,9 +704,9 @@ __device__ __forceinline__ void aff_dual_pass_nv(const AffArgs& a, const uint8_t
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
     if (MODE == kGlobal || nv == kRows || !last_pass)
-        return aff_dual_pass<MODE, CIGAR, kRows>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
+        return aff_dual_pass<MODE, CIGAR, kRows, CLS>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
 #define TA_NV_CASE(k) \
-    case k: return aff_dual_pass<MODE, CIGAR, k>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
+    case k: return aff_dual_pass<MODE, CIGAR, k, CLS>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -716,15 +728,20 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const uint8_t* Q[2];
     const uint8_t* T[2];
     uint2* ptrs[2];
-    bool tdash = false, qdash = false;
+    bool tdash = false, qdash = false, qother = false;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         Q[h] = a.qbytes + a.qoff[p[h]];
         T[h] = a.tbytes + a.toff[p[h]];
         ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
         for (uint32_t k = (uint32_t)lane; k < m; k += 64) tdash |= T[h][k] == '-';
-        for (uint32_t k = (uint32_t)lane; k < n; k += 64) qdash |= Q[h][k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < n; k += 64) {
+            const uint32_t c = Q[h][k];
+            qdash |= c == '-';
+            qother |= !is_acgt(c);
+        }
     }
+    const bool cls = __ballot(qother) == 0;
     if (__ballot(qdash)) {  // per-row vertical gap constants: the int32 fill takes the couple
         if (lane == 0) {
             const uint32_t at = atomicAdd(a.fb_count, 2u);
@@ -747,7 +764,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const bool last_pass = pass + 1 == passes;
         PassOut o[2];
-        aff_dual_pass_nv<MODE, CIGAR>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, o);
+        if (cls) aff_dual_pass_nv<MODE, CIGAR, true>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, o);
+        else aff_dual_pass_nv<MODE, CIGAR, false>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, o);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (MODE == kSemi && o[h].h > best_h[h]) {  // strict: the upper pass wins ties

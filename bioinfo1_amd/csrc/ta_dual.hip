@@ -166,6 +166,13 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
             uint32_t upv = recv;
             uint32_t Z = Zp;
+            // M3: the clamp bases of rows 2k, 2k+1 in the halves of W[k] (op_sel picks one)
+            uint32_t W[R / 2];
+            if constexpr (M3) {
+                W[0] = pk_sub(Zp, 0x00010000u);
+#pragma unroll
+                for (int k = 1; k < R / 2; ++k) W[k] = pk_sub(W[0], rep16(2 * k));
+            }
             static_for<0, R>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
                 const uint32_t old = H2[r];
@@ -175,7 +182,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 const uint32_t up = pk_add(upv, GUG);
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv;
-                if constexpr (M3) hv = pk_max3_pos(m1, up, Z);  // clamp folded in, :185
+                if constexpr (M3) hv = pk_max3_pos_bc<r & 1>(m1, up, W[r / 2]);  // clamp folded in, :185
                 else hv = LOCAL ? pk_max(pk_max(m1, up), Z) : pk_max(m1, up);
                 if (CIGAR) {
                     // raw compares (D wins over I in the walk; local walks track the
@@ -187,7 +194,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 }
                 H2[r] = hv;
                 upv = hv;
-                if (LOCAL && r + 1 < R) Z = pk_sub(Z, ONE);
+                if (LOCAL && !M3 && r + 1 < R) Z = pk_sub(Z, ONE);
             });
             if (LOCAL) {
                 // balanced trees (a serial packed-max chain stalls one cycle per link)

@@ -37,6 +37,14 @@ __device__ __forceinline__ uint32_t pk_max3_pos(uint32_t a, uint32_t b, uint32_t
     const h2v x = __builtin_bit_cast(h2v, a), y = __builtin_bit_cast(h2v, b), z = __builtin_bit_cast(h2v, c);
     return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), z));
 }
+// pk_max3_pos(a, b, one half of w in both halves): the broadcast folds into
+// the instruction's op_sel (two rows' clamp bases share one register)
+template <int HALF>
+__device__ __forceinline__ uint32_t pk_max3_pos_bc(uint32_t a, uint32_t b, uint32_t w) {
+    const h2v x = __builtin_bit_cast(h2v, a), y = __builtin_bit_cast(h2v, b), z = __builtin_bit_cast(h2v, w);
+    const h2v zz = __builtin_shufflevector(z, z, HALF, HALF);
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_maximum(__builtin_elementwise_maximum(x, y), zz));
+}
 // max over v[0..N) of such values: triples per level, ceil((N-1)/2) instructions
 template <int N>
 __device__ __forceinline__ uint32_t max3_reduce(const uint32_t* v) {
