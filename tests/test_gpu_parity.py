@@ -403,6 +403,40 @@ def test_local_group_walk_dual_and_fallback(aligner, oracle, sc):
             assert got.cigar(p) == want.cigar(p), (sc, flags, p)
 
 
+def test_local_walk_long_runs(aligner, oracle):
+    """Local paths with long gap and match runs (past the group walk's 32-cell
+    clip and the one-pair walk's 64-cell windows) across pass and tile edges
+    (1,100 x 1,100 pairs: two query passes); equal shapes so the couples run packed."""
+    rng = np.random.default_rng(0x1046)
+    al = np.frombuffer(b"ACGT", np.uint8)
+    pairs = []
+    for k in range(64):
+        core = al[rng.integers(4, size=300)].tobytes()
+        ins = b"N" * (40 + (k % 7) * 11)  # matches nothing: one contiguous gap run
+        if k % 2:  # a long insertion in the target (I run), then a long deletion (D runs)
+            q = core[:150] + core[150:]
+            t = core[:150] + ins + core[150:]
+        else:
+            q = core[:120] + ins + core[120:]
+            t = core
+        pad = 1100 - len(q), 1100 - len(t)
+        pairs.append((q + al[rng.integers(4, size=pad[0])].tobytes(), t + al[rng.integers(4, size=pad[1])].tobytes()))
+    b = synth.from_pairs(pairs)
+    for sc in ((5, -4, -1), (2, -3, -1)):
+        want = oracle.align_batch(b, 1, *sc, True)
+        for flags in (0, TA_PLAN_WALK1):
+            got = run_plan(aligner, b, 1, sc, True, flags)
+            np.testing.assert_array_equal(got.scores, want.scores)
+            np.testing.assert_array_equal(got.target_begins, want.target_begins)
+            for p in range(b.n_pairs):
+                assert got.cigar(p) == want.cigar(p), (sc, flags, p)
+    import re
+
+    runs = [(int(c), op) for p in range(b.n_pairs) for c, op in re.findall(rb"(\d+)([MID])", want.cigar(p))]
+    assert max(c for c, op in runs if op == b"I") > 32 and max(c for c, op in runs if op == b"D") > 32
+    assert max(c for c, op in runs if op == b"M") > 64
+
+
 def test_config5_shape_multichunk(aligner):
     """Config 5 shape forced through >= 4 chunks (small workspace budget):
     every chunk reuses the code workspace; the first 32 pairs bit-exact vs the
