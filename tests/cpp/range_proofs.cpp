@@ -1,0 +1,82 @@
+// tests/cpp/range_proofs.cpp -- brute-force check of the range bounds the
+// packed local fills rely on for their three-input max on f16 bit patterns
+// (every value must stay in [0, 0x7BFF]):
+//   * local_max3_offset (ta_layout.h, ta_dual.hip): S = 16H + z*j - i (z = 1 - 16 ma)
+//     plus the offset, for every cell of every row up to n + 15 (the last lane's
+//     padding rows) and every candidate (diag / left / up before the max);
+//   * flex_local_fits (ta_planner.cpp, ta_flex.hip): H itself is bounded by the
+//     planner's hmax for every cell (the rest of that bound is drift arithmetic).
+// The DP is the reference's local recurrence (team_alignment.cpp:171-194) on
+// random bytes ('-' in targets, whose gap steps are free).  Prints "ok" or the
+// first violation; exit status 0 / 1.
+#include <algorithm>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "ta_layout.h"
+#include "ta_planner.h"
+
+static int match_s(char a, char b, int ma, int mi) { return a == b ? ma : mi; }
+static int indel_s(char c, int gap) { return c == '-' ? 0 : gap; }
+
+int main(int argc, char** argv) {
+    const int iters = argc > 1 ? std::atoi(argv[1]) : 3000;
+    std::mt19937 rng(0x3A11);
+    // queries never hold '-' in the packed fills (those couples go to the int32 fill)
+    const char qalpha[] = "ACGTNa", talpha[] = "ACGT-N";
+    long checked = 0, dual_cases = 0, flex_cases = 0;
+    for (int it = 0; it < iters; ++it) {
+        const uint32_t big = (it % 10 == 0) ? 2000 : 90;  // every tenth near the bounds' limits
+        const uint32_t n = 1 + rng() % big, m = 1 + rng() % big;
+        const int ma = (int)(rng() % 9) - 2, mi = (int)(rng() % 9) - 6, gap = (int)(rng() % 7) - 4;
+        const int na = 2 + rng() % 5;  // alphabet size: more matches when small
+        std::string q(n + 16, 'A'), t(m, 'A');
+        for (auto& c : q) c = qalpha[rng() % na];
+        for (auto& c : t) c = talpha[rng() % na];
+        const int off = ta::local_max3_offset(n, m, ma, mi, gap);
+        const bool flex = ta::flex_local_fits(n, m, ma, mi, gap);
+        if (off < 0 && !flex) continue;
+        dual_cases += off >= 0;
+        flex_cases += flex;
+        // rows up to n + 15: the padding rows compute on whatever bytes sit there
+        const uint32_t N = n + 15;
+        std::vector<long> H((N + 1) * (m + 1), 0);
+        auto at = [&](uint32_t i, uint32_t j) -> long& { return H[(size_t)i * (m + 1) + j]; };
+        const long z = 1 - 16L * ma;
+        long hmax_pl = (long)std::min(n, m) * std::max({0, ma, mi}) + ((long)n + m) * std::max(0, gap);
+        for (uint32_t i = 1; i <= N; ++i)
+            for (uint32_t j = 1; j <= m; ++j) {
+                const long d = at(i - 1, j - 1) + match_s(q[i - 1], t[j - 1], ma, mi);
+                const long l = at(i, j - 1) + indel_s(t[j - 1], gap);
+                const long u = at(i - 1, j) + indel_s(q[i - 1], gap);
+                long h = d;
+                if (l > h) h = l;
+                if (u > h) h = u;
+                if (h < 0) h = 0;
+                at(i, j) = h;
+                if (off >= 0) {
+                    // S of the cell and of each candidate (same row/column offset)
+                    for (long cand : {d, l, u, h}) {
+                        const long s = 16 * cand + z * (long)j - (long)i + off;
+                        ++checked;
+                        if (s < 0 || s > 0x7BFF) {
+                            std::printf("max3 offset violated: n=%u m=%u sc=%d,%d,%d i=%u j=%u cand=%ld S'=%ld off=%d\n",
+                                        n, m, ma, mi, gap, i, j, cand, s, off);
+                            return 1;
+                        }
+                    }
+                }
+                if (flex && i <= n && h > hmax_pl) {
+                    std::printf("flex hmax violated: n=%u m=%u sc=%d,%d,%d H=%ld hmax=%ld\n", n, m, ma, mi, gap, h,
+                                hmax_pl);
+                    return 1;
+                }
+            }
+    }
+    std::printf("ok: %ld values (%ld max3-offset cases, %ld flex-local cases)\n", checked, dual_cases, flex_cases);
+    return 0;
+}
