@@ -28,6 +28,7 @@
 
 #include "ta_device.h"
 #include "ta_walk2.h"
+#include "ta_walk_lane.h"
 
 namespace ta {
 namespace {
@@ -420,6 +421,14 @@ __global__ __launch_bounds__(kBlock) void traceback_group_kernel(TraceArgs a) {
     traceback_group_local<G>(a, widx, threadIdx.x & 63);
 }
 
+// Local walks, one lane per pair stepping cell by cell, 64/G pairs per
+// one-wave block (ta_walk_lane.h).
+template <int G>
+__global__ __launch_bounds__(kWave) void traceback_lane_kernel(TraceArgs a) {
+    __shared__ uint32_t lds[(64 / G) * kLwGroupDw];
+    traceback_lane_local<G>(a, lds, (int)threadIdx.x);
+}
+
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
     const int lane = threadIdx.x & 63;
     const uint32_t p = wave_id();
@@ -455,6 +464,9 @@ hipError_t launch_fill_mode<TA_FILL_MODE, (TA_FILL_CIGAR != 0)>(bool wide, const
 #endif
 
 #ifdef TA_TU_MISC
+#ifndef TA_LW_G
+#define TA_LW_G 16
+#endif
 hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s) {
     switch (mode * 2 + (cigar ? 1 : 0)) {
         case 0: return launch_fill_mode<kGlobal, false>(wide, a, s);
@@ -498,6 +510,11 @@ hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int gro
         hipLaunchKernelGGL(traceback_group_kernel<32>, grid_for((a.count + 1) / 2), b, 0, s, a);
         return hipGetLastError();
     }
+    if (mode == kLocal && group == 16) {  // lane walks (TA_LW_G lanes per pair)
+        constexpr int W = 64 / TA_LW_G;
+        hipLaunchKernelGGL(traceback_lane_kernel<TA_LW_G>, dim3((a.count + W - 1) / W), dim3(kWave), 0, s, a);
+        return hipGetLastError();
+    }
     switch (mode) {
         case kGlobal: hipLaunchKernelGGL(traceback_kernel<kGlobal>, g, b, 0, s, a); break;
         case kLocal: hipLaunchKernelGGL(traceback_kernel<kLocal>, g, b, 0, s, a); break;
@@ -506,6 +523,17 @@ hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int gro
     }
     return hipGetLastError();
 }
+
+#ifdef TA_LW_PROF
+extern "C" int ta_lw_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(lw_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(lw_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
     if (!a.n_pairs) return hipSuccess;

@@ -293,14 +293,18 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     // A fill kernel that walks its own pair only pays when nothing else of the
     // chunk runs in the separate traceback kernel anyway.
     pl.fused = want_cigar && pl.n_dual_pairs == 0 && !(flags & kPlanUnfused);
-    // Local walks, two pairs per wave (32 lanes each, ta_walk2.h): 0.65 vs 0.77 ms on
-    // config 2 (16 lanes each: 0.75, too few waves to hide latency).  Their runs are
-    // clipped to 32 cells, so batches of long pairs (long M runs) keep the one-pair
-    // walk (config 3 local: 4.1 vs 6.3 ms).  24-bit multiplies of the scores.
+    // Local walks of short pairs: lane walks (one lane per pair steps cell by cell
+    // through LDS tiles, ta_walk_lane.h; indel costs kept as int8).  Two pairs per
+    // wave (32 lanes each, ta_walk2.h): 0.65 vs 0.77 ms for one pair per wave on
+    // config 2; their runs are clipped to 32 cells, so batches of long pairs (long
+    // M runs) keep the one-pair walk (config 3 local: 4.1 vs 6.3 ms).  24-bit
+    // multiplies of the scores in the run walks.
     uint64_t len_sum = 0;
     for (uint32_t p = 0; p < n_pairs; ++p) len_sum += (uint64_t)qlen[p] + tlen[p];
     const bool short_pairs = len_sum <= 6000ull * std::max<uint32_t>(n_pairs, 1);
-    pl.walk_group = ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) ? 0 : 32;
+    if ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) pl.walk_group = 0;
+    else if ((flags & kPlanWalk2) || gap < -128 || gap > 127) pl.walk_group = 32;
+    else pl.walk_group = 16;
     // (Each dual wave walking its own two pairs right after its fill measured
     // slower: config 2 3.10 ms vs 2.19 + 0.65; the walk inherits the fill's
     // register allocation and all waves finish their fills together anyway.)

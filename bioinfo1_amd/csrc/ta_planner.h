@@ -18,7 +18,8 @@ namespace ta {
 constexpr uint32_t kPlanInt32Only = 1u;  // no packed two-pair kernels
 constexpr uint32_t kPlanNoFlex = 2u;     // no rebased (different-shape) couples
 constexpr uint32_t kPlanUnfused = 4u;    // int32-only plans: traceback as its own kernel
-constexpr uint32_t kPlanWalk1 = 8u;      // local walks one pair per wave (not two, ta_walk2.h)
+constexpr uint32_t kPlanWalk1 = 8u;      // local walks: one pair per wave (traceback_pair)
+constexpr uint32_t kPlanWalk2 = 16u;     // local walks: two pairs per wave (ta_walk2.h), not lane walks
 
 // Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
@@ -36,7 +37,9 @@ struct Plan {
     bool want_cigar = false;
     bool wide = false;   // local mode with |values| that could reach 2^25: unscaled int32 kernel
     bool fused = false;  // int32-only plans: the fill kernel walks its own pair
-    int walk_group = 32;  // local walks: lanes per pair (traceback_group_kernel), 0 = one pair per wave
+    // local walks: 16 = lane walks (ta_walk_lane.h), 32 = two pairs per wave
+    // (ta_walk2.h), 0 = one pair per wave (traceback_pair)
+    int walk_group = 16;
     std::vector<uint32_t> qlen, tlen;
     std::vector<uint32_t> order;    // traceback order (all pairs)
     std::vector<uint32_t> singles;  // int32 fill: pair ids

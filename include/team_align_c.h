@@ -105,7 +105,8 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, c
 #define TA_PLAN_INT32_ONLY 1u /* no packed two-pairs-per-wave int16 kernels */
 #define TA_PLAN_NO_FLEX 2u    /* no rebased couples of different shapes */
 #define TA_PLAN_UNFUSED 4u    /* int32-only plans: traceback as its own kernel, not inside the fill */
-#define TA_PLAN_WALK1 8u      /* local tracebacks: one pair per wave instead of two */
+#define TA_PLAN_WALK1 8u      /* local tracebacks: one pair per wave (run walk) */
+#define TA_PLAN_WALK2 16u     /* local tracebacks: two pairs per wave (run walk), not one lane per pair */
 int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
                    const uint32_t* target_len_host, int type, int match, int mismatch, int gap, int want_cigar,
                    uint64_t workspace_budget, uint32_t flags, ta_plan** out);

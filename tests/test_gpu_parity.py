@@ -9,7 +9,7 @@ import pytest
 from conftest import DIGESTS, ROOT, cigar_digest, digest_batch, load_digest, run_plan
 
 from bioinfo1_amd import synth
-from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, Aligner, DevicePlan,
+from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2, Aligner, DevicePlan,
                                 align)
 from oracle.pyoracle import Oracle
 
@@ -144,7 +144,7 @@ def test_dual_fuzz(aligner, oracle, case):
     plan.close()
     want = oracle.align_batch(b, mode, *sc, True)
     # packed kernels (default), the int32 kernel alone (fused / separate walk)
-    for flags in (0, TA_PLAN_WALK1, TA_PLAN_INT32_ONLY, TA_PLAN_INT32_ONLY | TA_PLAN_UNFUSED):
+    for flags in (0, TA_PLAN_WALK1, TA_PLAN_WALK2, TA_PLAN_INT32_ONLY, TA_PLAN_INT32_ONLY | TA_PLAN_UNFUSED):
         for cig in (True, False):
             got = run_plan(aligner, b, mode, sc, cig, flags)
             np.testing.assert_array_equal(got.scores, want.scores)
@@ -395,7 +395,7 @@ def test_local_group_walk_dual_and_fallback(aligner, oracle, sc):
     assert plan.dual_pairs == 96 and not plan.fused, (plan.dual_pairs, plan.fused)
     plan.close()
     want = oracle.align_batch(b, 1, *sc, True)
-    for flags in (0, TA_PLAN_WALK1):
+    for flags in (0, TA_PLAN_WALK1, TA_PLAN_WALK2):
         got = run_plan(aligner, b, 1, sc, True, flags)
         np.testing.assert_array_equal(got.scores, want.scores)
         np.testing.assert_array_equal(got.target_begins, want.target_begins)
@@ -424,7 +424,7 @@ def test_local_walk_long_runs(aligner, oracle):
     b = synth.from_pairs(pairs)
     for sc in ((5, -4, -1), (2, -3, -1)):
         want = oracle.align_batch(b, 1, *sc, True)
-        for flags in (0, TA_PLAN_WALK1):
+        for flags in (0, TA_PLAN_WALK1, TA_PLAN_WALK2):
             got = run_plan(aligner, b, 1, sc, True, flags)
             np.testing.assert_array_equal(got.scores, want.scores)
             np.testing.assert_array_equal(got.target_begins, want.target_begins)
@@ -543,3 +543,23 @@ def test_flex_local_no_positive_cell(aligner, oracle):
     np.testing.assert_array_equal(got.scores, want.scores)
     np.testing.assert_array_equal(got.target_begins, want.target_begins)
     assert got.cigars() == want.cigars()
+
+
+def test_local_walk_choices(aligner, oracle):
+    """Local walks of every kind on the same batches: lane walks (default for
+    short pairs with an int8 gap), two-pair run walks (TA_PLAN_WALK2, and the
+    default when |gap| > 127), one-pair run walks (TA_PLAN_WALK1); '-' bytes
+    make indel steps free (the lane walk's per-byte indel costs)."""
+    rng = np.random.default_rng(0x1A2E)
+    for alpha, sc in ((b"ACGT", (1, -1, -1)), (b"AC-GT", (2, -1, 3)), (b"ACGT", (300, -200, -150)),
+                      (b"ACGTN-", (4, -3, -2))):
+        al = np.frombuffer(alpha, np.uint8)
+        pairs = [(al[rng.integers(len(al), size=int(rng.integers(1, 700)))].tobytes(),
+                  al[rng.integers(len(al), size=int(rng.integers(1, 700)))].tobytes()) for _ in range(150)]
+        b = synth.from_pairs(pairs)
+        want = oracle.align_batch(b, 1, *sc, True)
+        for flags in (0, TA_PLAN_WALK1, TA_PLAN_WALK2):
+            got = run_plan(aligner, b, 1, sc, True, flags)
+            np.testing.assert_array_equal(got.scores, want.scores)
+            for p in range(b.n_pairs):
+                assert got.cigar(p) == want.cigar(p), (alpha, sc, flags, p)
