@@ -47,7 +47,7 @@ struct DualIo {
 // (ta_packed.h mismatch_table / row_selector), one v_perm per row.
 template <int MODE, bool CIGAR, int NV, bool M3, bool CLS>
 __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
-                                             uint32_t pass, bool last_pass, bool tdash, int lane, int off = 0) {
+                                             uint32_t pass, bool last_pass, int lane, int off = 0) {
     constexpr int R = kRows;
     constexpr bool LOCAL = MODE == kLocal;
     static_assert(!M3 || LOCAL, "three-input maxima: local mode only");
@@ -56,8 +56,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     const int init = (MODE == kGlobal) ? gap : 0;
     const int zstep = 1 - 16 * ma;  // local: S(0, j) = zstep * j
     const uint32_t KD = rep16(LOCAL ? 16 * (mi - ma) : (mi - ma));
-    const int glg = LOCAL ? 16 * gap + zstep : gap - ma;  // left gain, target byte != '-'
-    const int gld = LOCAL ? zstep : -ma;                  // left gain, target byte == '-'
+    const uint32_t GL = rep16(LOCAL ? 16 * gap + zstep : gap - ma);  // left gain (no '-' in these targets)
     const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : gap);  // up gain (no '-' in these queries)
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16 (see pk_min_u16)
@@ -99,17 +98,20 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         tcur[h] = load_tchunk(io.T[h], m, 0, lane);
         tnext[h] = load_tchunk(io.T[h], m, 1, lane);
     }
-    int bcur = 0, bnext = 0;
-    if (pass > 0) {
-        bcur = load_bchunk(io.B, m, 0, lane);
-        bnext = load_bchunk(io.B, m, 1, lane);
-    }
+    // The row above the pass, 64 columns per chunk (lane k: column 64c + k + 1):
+    // the boundary row S(0, j) in pass 0, the previous pass's bottom row after.
+    auto top_chunk = [&](uint32_t c) -> int {
+        if (pass > 0) return load_bchunk(io.B, m, c, lane);
+        const int j = (int)(c * 64u + (uint32_t)lane + 1u);
+        return (int)rep16(LOCAL ? off + zstep * j : (init - ma) * j);
+    };
+    int bcur = top_chunk(0), bnext = top_chunk(1);
     const uint32_t steps = m + nl - 1;
     uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * Tmax * kWave : nullptr;
     uint32_t* prow1 = CIGAR ? io.ptrs[1] + (uint64_t)pass * Tmax * kWave : nullptr;
 
-    // Chunk reloads (every 256 steps: target bytes; every 64: the boundary
-    // row of a later pass) are hoisted out of the step loop by run_steps.
+    // Chunk reloads (every 256 steps: target bytes; every 64: the row above)
+    // are hoisted out of the step loop by run_steps.
     auto reload = [&](uint32_t t) {
         if ((t & 255u) == 0) {
 #pragma unroll
@@ -118,19 +120,12 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 tnext[h] = load_tchunk(io.T[h], m, (t >> 8) + 1, lane);
             }
         }
-        if (pass > 0) {
-            bcur = bnext;
-            bnext = load_bchunk(io.B, m, (t >> 6) + 1, lane);
-        }
+        bcur = bnext;
+        bnext = top_chunk((t >> 6) + 1);
     };
     auto step = [&](uint32_t t, auto masked_tag) {
         constexpr bool MASKED = decltype(masked_tag)::value;
-        uint32_t top;
-        if (pass == 0) {
-            top = rep16(LOCAL ? off + zstep * (int)(t + 1) : (init - ma) * (int)(t + 1));  // S(0, j)
-        } else {
-            top = (uint32_t)rdlane(bcur, t & 63u);
-        }
+        const uint32_t top = (uint32_t)rdlane(bcur, t & 63u);
         const uint32_t sh = (t & 3u) * 8;
         const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
         const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
@@ -140,7 +135,6 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         if constexpr (CLS) {
             tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
             tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
-            if (tdash) tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
         } else {
             tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
         }
@@ -153,12 +147,6 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         // rows 0-7 / 8-15: bytes [I_A, I_B, D_A, D_B], row r at bit 7 - r%8
         uint32_t acc0 = 0, acc1 = 0;
         if (active) {
-            uint32_t GL = rep16(glg);
-            if (tdash) {
-                const int ga = ((tc2 & 0xFFFFu) == '-') ? gld : glg;
-                const int gb = ((tc2 >> 16) == '-') ? gld : glg;
-                GL = ((uint32_t)ga & 0xFFFFu) | ((uint32_t)gb << 16);
-            }
             auto e_of = [&](int r) {  // 0 on a match, 1 otherwise
                 if constexpr (CLS) return mismatch_flags(tA, tB, q2[r]);
                 else return pk_min_u16(q2[r] ^ tc2, ONE);
@@ -232,16 +220,21 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         }
     };
     const uint32_t ramp_end = min(nl - 1, steps);
-    const uint32_t every = (pass > 0) ? 64u : 256u;
-    uint32_t t = 0, next_reload = every;
+    uint32_t t = 0, next_reload = 64;
+    // Steps in pairs: the loop-carried DPP registers alternate between the two
+    // copies instead of being copied back every step.
     auto run_steps = [&](uint32_t t_end, auto masked_tag) {
         while (t < t_end) {
             if (t == next_reload) {
                 reload(t);
-                next_reload += every;
+                next_reload += 64;
             }
             const uint32_t blk = min(t_end, next_reload);
-            for (; t < blk; ++t) step(t, masked_tag);
+            for (; t + 1 < blk; t += 2) {
+                step(t, masked_tag);
+                step(t + 1, masked_tag);
+            }
+            if (t < blk) step(t++, masked_tag);
         }
     };
     run_steps(ramp_end, std::true_type{});
@@ -298,16 +291,16 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
 
 template <int MODE, bool CIGAR, bool CLS>
 __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
-                                                uint32_t pass, bool last_pass, bool tdash, int lane) {
+                                                uint32_t pass, bool last_pass, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
     if constexpr (MODE == kLocal) {
         const int off = local_max3_offset(n, m, a.match, a.mismatch, a.gap);  // wave-uniform
         if (off >= 0) {
             if (nv == kRows)
-                return dual_pass<MODE, CIGAR, kRows, true, CLS>(a, io, n, m, pass, last_pass, tdash, lane, off);
+                return dual_pass<MODE, CIGAR, kRows, true, CLS>(a, io, n, m, pass, last_pass, lane, off);
 #define TA_NV_CASE(k) \
-    case k: return dual_pass<MODE, CIGAR, k, true, CLS>(a, io, n, m, pass, last_pass, tdash, lane, off);
+    case k: return dual_pass<MODE, CIGAR, k, true, CLS>(a, io, n, m, pass, last_pass, lane, off);
             switch (nv) {
                 TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
                 TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -317,9 +310,9 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
         }
     }
     if (MODE == kGlobal || nv == kRows)
-        return dual_pass<MODE, CIGAR, kRows, false, CLS>(a, io, n, m, pass, last_pass, tdash, lane);
+        return dual_pass<MODE, CIGAR, kRows, false, CLS>(a, io, n, m, pass, last_pass, lane);
 #define TA_NV_CASE(k) \
-    case k: return dual_pass<MODE, CIGAR, k, false, CLS>(a, io, n, m, pass, last_pass, tdash, lane);
+    case k: return dual_pass<MODE, CIGAR, k, false, CLS>(a, io, n, m, pass, last_pass, lane);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -345,24 +338,26 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     p[1] = a.order[2 * (a.begin + widx) + 1];
     const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
     DualIo io;
-    bool tdash = false, qdash = false, qother = false;
+    bool dash = false, qother = false;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         io.Q[h] = a.qbytes + a.qoff[p[h]];
         io.T[h] = a.tbytes + a.toff[p[h]];
         io.ptrs[h] = CIGAR ? a.ptrs + a.ptr_off[p[h]] : nullptr;
-        for (uint32_t k = (uint32_t)lane; k < m; k += 64) tdash |= io.T[h][k] == '-';
+        for (uint32_t k = (uint32_t)lane; k < m; k += 64) dash |= io.T[h][k] == '-';
         for (uint32_t k = (uint32_t)lane; k < n; k += 64) {
             const uint32_t c = io.Q[h][k];
-            qdash |= c == '-';
+            dash |= c == '-';
             qother |= !is_acgt(c);
         }
     }
     const bool cls = __ballot(qother) == 0;  // queries of A, C, G, T only: table mismatch flags
-    // A '-' in a query changes the up gain per row; that variant would cost
-    // this kernel ~30 VGPRs for input real reads never contain, so such
-    // couples go to the int32 fill (launched right after, same workspace).
-    if (__ballot(qdash)) {
+    // A '-' (a free gap step, team_alignment.cpp:25-28) changes the up gain per
+    // row (query) or the left gain per step (target); those variants would cost
+    // this kernel ~30 VGPRs and per-step selects for input real reads never
+    // contain, so such couples go to the int32 fill (launched right after,
+    // same workspace).
+    if (__ballot(dash)) {
         if (lane == 0) {
             const uint32_t at = atomicAdd(a.fb_count, 2u);
             a.fb_list[at] = p[0];
@@ -370,7 +365,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
         }
         return;
     }
-    tdash = __ballot(tdash) != 0;
     const uint32_t passes = n_passes(n);
     io.B = (passes > 1) ? a.bnd + a.bnd_off[p[0]] : nullptr;
     int best_h[2], corner[2] = {0, 0};
@@ -383,8 +377,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     }
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const bool last_pass = pass + 1 == passes;
-        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, pass, last_pass, tdash, lane)
-                              : dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, pass, last_pass, tdash, lane);
+        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, pass, last_pass, lane)
+                              : dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, pass, last_pass, lane);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (MODE != kGlobal && o.o[h].h > best_h[h]) {
