@@ -65,6 +65,14 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
     const uint32_t nl = (nrows + R - 1) / R;
     const bool has_next = !last_pass;
+    // UZ (with M3): lane l keeps its values in the frame S + dl*l (dl = zstep + 16),
+    // which makes the clamp base of a step the same in every lane: the bases
+    // and the argmax column then live in SGPRs (SALU work) instead of VALU
+    // registers, for one packed add per step on the value handed down (each
+    // hand-off crosses one lane).  local_max3_offset bounds the frame too.
+    constexpr bool UZ = M3;
+    const int dl = UZ ? zstep + 16 : 0;
+    const uint32_t D2 = rep16(dl);
 
     uint32_t q2[R], H2[R];
 #pragma unroll
@@ -72,10 +80,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
         if constexpr (CLS) q2[r] = i0 < n ? row_selector(io.Q[0][i0], io.Q[1][i0]) : row_selector(0, 0);
         else q2[r] = i0 < n ? ((uint32_t)io.Q[0][i0] | ((uint32_t)io.Q[1][i0] << 16)) : 0u;
-        H2[r] = rep16(LOCAL ? off - (int)(i0 + 1) : wmul(i0 + 1, init));  // S(i, 0)
+        H2[r] = rep16(LOCAL ? off - (int)(i0 + 1) + dl * lane : wmul(i0 + 1, init));  // S(i, 0)
     }
     const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
-    uint32_t recv = rep16(LOCAL ? off - (int)ia : wmul(ia, init));
+    uint32_t recv = rep16(LOCAL ? off - (int)ia + dl * lane : wmul(ia, init));
     uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
     const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
     // Per-lane running values, both pairs packed, advanced once per step:
@@ -85,6 +93,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // of a saturating packed difference, spread over its half by v_perm,
     // selects the new column with one v_bfi; the value is a packed max.
     uint32_t Zp = rep16(off + zstep * (0 - lane) - (int)(ia + 1));
+    int zu = off - (int)row_base - 1;  // UZ: the clamp base of row 0 in the lane frame (t = -1)
     const uint32_t ZS2 = rep16(zstep);
     uint32_t jj = rep16(-lane), maj = rep16(-ma * lane);
     const uint32_t MA2 = rep16(ma);
@@ -100,10 +109,11 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     }
     // The row above the pass, 64 columns per chunk (lane k: column 64c + k + 1):
     // the boundary row S(0, j) in pass 0, the previous pass's bottom row after.
+    // UZ: minus dl, which the hand-off adds back in lane 0 too.
     auto top_chunk = [&](uint32_t c) -> int {
-        if (pass > 0) return load_bchunk(io.B, m, c, lane);
+        if (pass > 0) return (int)pk_sub((uint32_t)load_bchunk(io.B, m, c, lane), D2);
         const int j = (int)(c * 64u + (uint32_t)lane + 1u);
-        return (int)rep16(LOCAL ? off + zstep * j : (init - ma) * j);
+        return (int)rep16(LOCAL ? off + zstep * j - dl : (init - ma) * j);
     };
     int bcur = top_chunk(0), bnext = top_chunk(1);
     const uint32_t steps = m + nl - 1;
@@ -132,14 +142,19 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
         const uint32_t prev = recv;
         recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
+        if constexpr (UZ) recv = pk_add(recv, D2);
         if constexpr (CLS) {
             tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
             tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
         } else {
             tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
         }
-        Zp = pk_add(Zp, ZS2);
-        jj = pk_add(jj, ONE);
+        if constexpr (UZ) {
+            zu += zstep;
+        } else {
+            Zp = pk_add(Zp, ZS2);
+            jj = pk_add(jj, ONE);
+        }
         if (MODE == kSemi) maj = pk_add(maj, MA2);
 
         const int j = (int)t - lane + 1;
@@ -157,9 +172,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             // M3: the clamp bases of rows 2k, 2k+1 in the halves of W[k] (op_sel picks one)
             uint32_t W[R / 2];
             if constexpr (M3) {
-                W[0] = pk_sub(Zp, 0x00010000u);
+                // wave-uniform (SALU): halves zu - 2k, zu - 2k - 1, all >= 0 (no borrows)
+                W[0] = ((uint32_t)zu & 0xFFFFu) * 0x10001u - 0x10000u;
 #pragma unroll
-                for (int k = 1; k < R / 2; ++k) W[k] = pk_sub(W[0], rep16(2 * k));
+                for (int k = 1; k < R / 2; ++k) W[k] = W[0] - 0x20002u * (uint32_t)k;
             }
             static_for<0, R>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
@@ -200,16 +216,24 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                     sk = ((uint32_t)lane == nl - 1) ? lo : full;
                 }
                 // key = S - Zb = 16H - r per half; strict '>' keeps the first column (:186)
-                const uint32_t key = pk_sub(sk, Zp);
-                bestj = bfi(half_mask(pk_sub_sat(bestK, key)), jj, bestj);
-                bestK = pk_max(bestK, key);
+                if constexpr (UZ) {
+                    // the column as the step t + 1 (uniform); j = t + 1 - lane at the end
+                    const uint32_t key = pk_sub(sk, ((uint32_t)zu & 0xFFFFu) * 0x10001u);
+                    const uint32_t msk = half_mask(pk_sub_sat(bestK, key));
+                    bestj = (((t + 1u) * 0x10001u) & msk) | (bestj & ~msk);
+                    bestK = pk_max(bestK, key);
+                } else {
+                    const uint32_t key = pk_sub(sk, Zp);
+                    bestj = bfi(half_mask(pk_sub_sat(bestK, key)), jj, bestj);
+                    bestK = pk_max(bestK, key);
+                }
             }
             if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + ma*j, strict '>' (:271-278)
                 const uint32_t v = pk_add(H2[NV - 1], maj);
                 rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jj, rowbest_j);
                 rowbest = pk_max(rowbest, v);
             }
-            if (has_next && (uint32_t)lane == nl - 1) io.B[j] = (int32_t)H2[R - 1];
+            if (has_next && (uint32_t)lane == nl - 1) io.B[j] = (int32_t)(UZ ? pk_sub(H2[R - 1], rep16(dl * lane)) : H2[R - 1]);
         }
         if (CIGAR) {
             // per pair: [I rows 8-15, I rows 0-7, D rows 8-15, D rows 0-7] (ta_internal.h Code)
@@ -252,7 +276,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             const int mx = wave_max(v);
             const int fl = first_lane(v == mx);
             const int Kf = rdlane(K, fl);
-            const uint32_t jf = (uint32_t)rdlane((int)(h ? (bestj >> 16) : (bestj & 0xFFFFu)), fl);
+            const uint32_t jf = (uint32_t)rdlane((int)(h ? (bestj >> 16) : (bestj & 0xFFFFu)), fl) - (UZ ? (uint32_t)fl : 0u);
             o.h = mx;
             o.i = row_base + (uint32_t)fl * R + (uint32_t)(15 - (Kf & 15)) + 1;
             o.j = jf;

@@ -33,7 +33,9 @@ enum Mode : int { kGlobal = 0, kLocal = 1, kSemi = 2 };
 //   H <= hs*j + gp*(i + j)   (hs = max(0, ma, mi), gp = max(0, gap))
 //   S <= (16hs + 16gp + z)*j + (16gp - 1)*i,   S >= z*j - i (the clamp),
 // rows up to n + 15 (the last lane's padding rows), candidates one step
-// (<= 16*mag) below the clamp.  -1: does not fit (the max/max kernel runs).
+// (<= 16*mag) below the clamp; lane l holds S + (z + 16)*l (its frame, so
+// that the clamp bases of a step are the same in every lane), l < 64.
+// -1: does not fit (the max/max kernel runs).
 TA_HD inline int local_max3_offset(uint32_t n, uint32_t m, int ma, int mi, int gap) {
     const long long N = (long long)n + 16, M = m;
     const long long ama = ma < 0 ? -ma : ma, ami = mi < 0 ? -mi : mi, ag = gap < 0 ? -gap : gap;
@@ -42,8 +44,9 @@ TA_HD inline int local_max3_offset(uint32_t n, uint32_t m, int ma, int mi, int g
     const long long gp = gap > 0 ? gap : 0;
     const long long z = 1 - 16LL * ma;
     const long long cj = 16 * hs + 16 * gp + z, ci = 16 * gp - 1;
-    const long long hi = (cj > 0 ? cj * M : 0) + (ci > 0 ? ci * N : 0) + 32 * (mag + 1);
-    const long long lo = (z < 0 ? z * M : 0) - N - 32 * (mag + 1);
+    const long long fl = 63 * (z + 16);  // lane frame
+    const long long hi = (cj > 0 ? cj * M : 0) + (ci > 0 ? ci * N : 0) + 32 * (mag + 1) + (fl > 0 ? fl : 0);
+    const long long lo = (z < 0 ? z * M : 0) - N - 32 * (mag + 1) + (fl < 0 ? fl : 0);
     if (hi - lo > 0x7BFF) return -1;
     return (int)(-lo);
 }

@@ -2,7 +2,7 @@
 // packed local fills rely on for their three-input max on f16 bit patterns
 // (every value must stay in [0, 0x7BFF]):
 //   * local_max3_offset (ta_layout.h, ta_dual.hip): S = 16H + z*j - i (z = 1 - 16 ma)
-//     plus the offset, for every cell of every row up to n + 15 (the last lane's
+//     plus the offset and the lane frame (z + 16) * lane, for every cell of every row up to n + 15 (the last lane's
 //     padding rows) and every candidate (diag / left / up before the max);
 //   * flex_local_fits (ta_planner.cpp, ta_flex.hip): H itself is bounded by the
 //     planner's hmax for every cell (the rest of that bound is drift arithmetic).
@@ -59,9 +59,11 @@ int main(int argc, char** argv) {
                 if (h < 0) h = 0;
                 at(i, j) = h;
                 if (off >= 0) {
-                    // S of the cell and of each candidate (same row/column offset)
+                    // S of the cell and of each candidate (same row/column offset), in
+                    // the frame of the lane that holds row i: + (z + 16) * lane
+                    const long lane = (long)(((i - 1) % 1024) / 16);
                     for (long cand : {d, l, u, h}) {
-                        const long s = 16 * cand + z * (long)j - (long)i + off;
+                        const long s = 16 * cand + z * (long)j - (long)i + off + (z + 16) * lane;
                         ++checked;
                         if (s < 0 || s > 0x7BFF) {
                             std::printf("max3 offset violated: n=%u m=%u sc=%d,%d,%d i=%u j=%u cand=%ld S'=%ld off=%d\n",
