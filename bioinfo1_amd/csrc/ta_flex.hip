@@ -337,7 +337,11 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 next_reload += 64;
             }
             const uint32_t blk = min(t_end, next_reload);
-            for (; t < blk; ++t) step(t, masked_tag);
+            for (; t + 1 < blk; t += 2) {  // steps in pairs (as ta_dual.hip)
+                step(t, masked_tag);
+                step(t + 1, masked_tag);
+            }
+            if (t < blk) step(t++, masked_tag);
         }
     };
     run_steps(ramp_end, std::true_type{});

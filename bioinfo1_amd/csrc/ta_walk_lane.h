@@ -38,6 +38,18 @@ __device__ unsigned long long lw_prof[8];
 #define LW_ACC(k, d)
 #endif
 
+// 32-bit LDS byte addresses (the group's arrays are LDS; keeps the cell
+// loop's address math in 32 bits)
+typedef __attribute__((address_space(3))) uint32_t lds_u32;
+typedef __attribute__((address_space(3))) uint16_t lds_u16;
+template <typename T>
+__device__ __forceinline__ uint32_t lds_addr(const T* p) {
+    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
+}
+__device__ __forceinline__ uint32_t lds_ld32(uint32_t a) { return *(const lds_u32*)(uintptr_t)a; }
+__device__ __forceinline__ uint32_t lds_ld16(uint32_t a) { return *(const lds_u16*)(uintptr_t)a; }
+__device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(lds_u32*)(uintptr_t)a = v; }
+
 constexpr int kLwStripes = 8;                          // tile rows: 8 stripes = 128 query rows
 constexpr int kLwSteps = 64;                           // tile columns: 64 steps of the pass
 constexpr int kLwRunCap = 64;                          // runs listed before a flush
@@ -143,16 +155,20 @@ __device__ __forceinline__ void lw_flush(const uint32_t* runs, int nflush, char*
         const bool act = e < nflush;
         const uint32_t v = act ? runs[e] : 0u;
         uint32_t c = v >> 2;
-        const uint32_t digits = 1u + (c >= 10u) + (c >= 100u) + (c >= 1000u) + (c >= 10000u) + (c >= 100000u) +
-                                (c >= 1000000u) + (c >= 10000000u) + (c >= 100000000u) + (c >= 1000000000u);
+        // counts below 65,536 (every run of pairs shorter than that): five digit
+        // tests and exact 24-bit reciprocal divisions, (c * 52429) >> 19 = c / 10
+        const bool big = ballot(c >= 65536u) != 0;
+        uint32_t digits = 1u + (c >= 10u) + (c >= 100u) + (c >= 1000u) + (c >= 10000u);
+        if (big)
+            digits += (c >= 100000u) + (c >= 1000000u) + (c >= 10000000u) + (c >= 100000000u) + (c >= 1000000000u);
         const uint32_t L = act ? digits + 1u : 0u;
         const uint32_t incl = (uint32_t)lw_prefix<G>((int)L, li);
         char* p = end - used - (incl - L) - 1;
         if (act) *p = (char)((0x44494Du >> (8u * (v & 3u))) & 0xFFu);  // 'M', 'I', 'D'
-#pragma unroll
-        for (uint32_t d = 0; d < 10u; ++d) {
-            if (d < digits && act) p[-1 - (int)d] = (char)('0' + c % 10u);
-            c /= 10u;
+        for (uint32_t d = 0; ballot(act && d < digits); ++d) {
+            const uint32_t q = big ? c / 10u : (__umul24(c, 52429u) >> 19);
+            if (act && d < digits) p[-1 - (int)d] = (char)('0' + (c - q * 10u));
+            c = q;
         }
         used += gread<G>(incl, h, G - 1);
     }
@@ -226,21 +242,25 @@ __device__ __forceinline__ void traceback_lane_local(const TraceArgs& a, uint32_
             // previous cell is written just before them (LDS completes in order),
             // and a cell whose successor provably stays inside the tile with a
             // positive cost and room in the run list (`safe`, from the state
-            // before the reads) skips the exact exit test.
+            // before the reads) skips the exact exit test.  32-bit LDS byte
+            // addresses (no 64-bit pointer math; full-rate 24-bit multiplies).
+            const uint32_t tb = lds_addr(tile), qb = lds_addr(qw), tcb = lds_addr(tw), rb = lds_addr(runs);
+            int mav = ma, miv = mi;  // held in VGPRs (a select reads at most one SGPR besides vcc)
+            asm volatile("" : "+v"(mav), "+v"(miv));
             while (true) {
-                runs[nr] = op | (cnt << 2);  // (every lane of the group: same value)
+                lds_st32(rb + 4u * (uint32_t)nr, op | (cnt << 2));  // (every lane of the group: same value)
                 const int s = lr >> 4;
-                const uint32_t code =
-                    *(const uint32_t*)((const char*)tile + (lc * 32 + s * 36 - 4 * kLwStripes * (kLwStripes - 1)));
-                const uint32_t qv = qw[lr], tv = tw[lc];
+                const uint32_t code = lds_ld32(tb + ((uint32_t)lc << 5) + __umul24((uint32_t)s, 36u) -
+                                               4u * kLwStripes * (kLwStripes - 1));
+                const uint32_t qv = lds_ld16(qb + ((uint32_t)lr << 1)), tv = lds_ld16(tcb + ((uint32_t)lc << 1));
                 const bool safe = H > posM && lr >= 1 && lc + s - (kLwStripes - 1) >= 2 && nr < kLwRunCap - 2;
                 // bit planes (ta_internal.h Code): row r's D bit at 31 - r, I bit at 15 - r
                 const uint32_t x = (code >> ((uint32_t)~lr & 15u)) & 0x10001u;
                 const uint32_t o = min(x, 2u);  // 0 M, 1 I, 2 D (D wins)
                 lr -= (o != 1u) ? 1 : 0;
                 lc -= (o != 2u) ? 1 : 0;
-                const int sm = ((qv & 0xFFu) == (tv & 0xFFu)) ? ma : mi;
-                const int sg = (int)(int8_t)(((o == 2u) ? qv : tv) >> 8);
+                const int sm = (((qv ^ tv) & 0xFFu) == 0u) ? mav : miv;
+                const int sg = __builtin_amdgcn_sbfe((int)((o == 2u) ? qv : tv), 8, 8);
                 H -= (o == 0u) ? sm : sg;
                 const bool same = o == op;
                 cnt = same ? cnt + 1u : 1u;
