@@ -73,6 +73,7 @@ def lib() -> C.CDLL:
     L.ta_cigar_slot_bytes.argtypes = [C.c_uint32, C.c_uint32]
     L.ta_align_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, u64p, u32p, C.c_void_p, u64p, u32p, C.c_int,
                                  C.c_int, C.c_int, C.c_int, C.c_int, i32p, u32p, C.c_void_p, C.c_uint64, u64p, u32p]
+    L.ta_align_batch_flags.argtypes = L.ta_align_batch.argtypes + [C.c_uint32]
     L.ta_context_release.argtypes = [C.c_void_p]
     L.ta_context_release.restype = None
     L.ta_context_held_bytes.argtypes = [C.c_void_p]
@@ -123,7 +124,7 @@ def lib() -> C.CDLL:
 ABI_SYMBOLS = [
     "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_context_release",
     "ta_context_held_bytes",
-    "ta_cigar_slot_bytes", "ta_align_batch", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes",
+    "ta_cigar_slot_bytes", "ta_align_batch", "ta_align_batch_flags", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes",
     "ta_plan_workspace_bytes", "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_fused",
     "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_execute_traceback", "ta_compact_cigars",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",

@@ -471,6 +471,15 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
                    const char* tbytes, const uint64_t* toff, const uint32_t* tlen, int type, int match,
                    int mismatch, int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* arena,
                    uint64_t arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len) {
+    return ta_align_batch_flags(ctx, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, type, match, mismatch, gap,
+                                want_cigar, score, target_begin, arena, arena_bytes, cigar_off, cigar_len, 0);
+}
+
+int ta_align_batch_flags(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff,
+                         const uint32_t* qlen, const char* tbytes, const uint64_t* toff, const uint32_t* tlen,
+                         int type, int match, int mismatch, int gap, int want_cigar, int32_t* score,
+                         uint32_t* target_begin, char* arena, uint64_t arena_bytes, uint64_t* cigar_off,
+                         uint32_t* cigar_len, uint32_t flags) {
     uint64_t qend = 0, tend = 0;
     if (int r = ta_host::check_host_batch(ctx, type, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, want_cigar, arena,
                                           cigar_off, cigar_len, &qend, &tend))
@@ -481,7 +490,7 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
     ta_plan pl;
     pl.ctx = ctx;
     ta::build_plan(pl.h, n_pairs, qlen, tlen, type, match, mismatch, gap, want_cigar != 0,
-                   ta_host::batch_budget(ctx, n_pairs, qlen, tlen, want_cigar, 4), 0, 4 * ctx->cu_count);
+                   ta_host::batch_budget(ctx, n_pairs, qlen, tlen, want_cigar, 4), flags, 4 * ctx->cu_count);
     LinearHostPlan hp(&pl);
     return ta_host::host_batch(ctx, hp, n_pairs, qb, qoff, qlen, tbytes, toff, tlen, qend, tend, want_cigar, score,
                                target_begin, arena, arena_bytes, cigar_off, cigar_len);

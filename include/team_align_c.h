@@ -93,6 +93,15 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, c
                    int32_t* score, uint32_t* target_begin, char* cigar_arena, uint64_t cigar_arena_bytes,
                    uint64_t* cigar_off, uint32_t* cigar_len);
 
+/* ta_align_batch with plan flags (TA_PLAN_* below: kernel selection, e.g.
+ * TA_PLAN_INT32_ONLY for one int32 wave per pair with its walk inside the
+ * fill kernel).  Results are identical for every flag value. */
+int ta_align_batch_flags(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, const uint64_t* query_off,
+                         const uint32_t* query_len, const char* target_bytes, const uint64_t* target_off,
+                         const uint32_t* target_len, int type, int match, int mismatch, int gap, int want_cigar,
+                         int32_t* score, uint32_t* target_begin, char* cigar_arena, uint64_t cigar_arena_bytes,
+                         uint64_t* cigar_off, uint32_t* cigar_len, uint32_t flags);
+
 /*
  * Device-resident batches (the mapper-side batching of SURVEY §8f and the
  * benchmark path).  A plan fixes the lengths (host arrays, copied) and the

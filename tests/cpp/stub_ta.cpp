@@ -68,4 +68,12 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
     return TA_OK;
 }
 
+int ta_align_batch_flags(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff,
+                         const uint32_t* qlen, const char* tb, const uint64_t* toff, const uint32_t* tlen, int type,
+                         int match, int mismatch, int gap, int want_cigar, int32_t* score, uint32_t* target_begin,
+                         char* arena, uint64_t arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len, uint32_t) {
+    return ta_align_batch(ctx, n_pairs, qb, qoff, qlen, tb, toff, tlen, type, match, mismatch, gap, want_cigar, score,
+                          target_begin, arena, arena_bytes, cigar_off, cigar_len);
+}
+
 }  // extern "C"
