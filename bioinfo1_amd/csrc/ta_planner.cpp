@@ -180,9 +180,18 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         // than the pipelined flexible fill on config 5, 4,056 vs 3,765 GCUPS)
         const bool couple = dual && k + 1 < n_pairs && qlen[order[k + 1]] == n && tlen[order[k + 1]] == m &&
                             fits_int16(type, n, m, match, mismatch, gap);
+        // A lone pair (one-pair batches: the drop-in call) runs coupled with
+        // itself in the packed kernel -- both halves compute it, its codes are
+        // written once -- whose wave and lane walk finish sooner than one int32
+        // wave walking inside the fill, except for tiny pairs where the one
+        // fused launch wins.
+        const bool self = dual && n_pairs == 1 && (uint64_t)n * m >= 4096 && fits_int16(type, n, m, match, mismatch, gap);
         if (couple) {
             units.push_back({1, p, order[k + 1], (uint64_t)n * m});
             k += 2;
+        } else if (self) {
+            units.push_back({1, p, p, (uint64_t)n * m});
+            ++k;
         } else {
             rest.push_back(p);
             ++k;
