@@ -88,14 +88,14 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
     // Per-lane running values, both pairs packed, advanced once per step:
     //   Zp = local clamp base Zb = zstep*j - (ia + 1) for this lane's column j
-    //   jj = j (= t - lane + 1);  maj = ma*j (semi: row n holds H = S + ma*j)
+    //   jj = j (= t - lane + 1); semi: row n holds H = S + ma*j
     // (all at t = -1 here).  Running bests are updated branch-free: the sign
     // of a saturating packed difference, spread over its half by v_perm,
     // selects the new column with one v_bfi; the value is a packed max.
     uint32_t Zp = rep16(off + zstep * (0 - lane) - (int)(ia + 1));
     int zu = off - (int)row_base - 1;  // UZ: the clamp base of row 0 in the lane frame (t = -1)
     const uint32_t ZS2 = rep16(zstep);
-    uint32_t jj = rep16(-lane), maj = rep16(-ma * lane);
+    uint32_t jj = rep16(-lane);
     const uint32_t MA2 = rep16(ma);
     // local: best key S - Zb = 16H - r (r = row in the stripe), -16 = no cell yet
     uint32_t bestK = rep16(-16), bestj = 0;
@@ -153,9 +153,8 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             zu += zstep;
         } else {
             Zp = pk_add(Zp, ZS2);
-            jj = pk_add(jj, ONE);
+            if (MODE != kSemi) jj = pk_add(jj, ONE);  // (semi: at its use, last pass only)
         }
-        if (MODE == kSemi) maj = pk_add(maj, MA2);
 
         const int j = (int)t - lane + 1;
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
@@ -229,8 +228,11 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 }
             }
             if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + ma*j, strict '>' (:271-278)
-                const uint32_t v = pk_add(H2[NV - 1], maj);
-                rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jj, rowbest_j);
+                // j and ma*j of this lane's column, formed here rather than carried
+                // through the passes that never read them
+                const uint32_t jl = rep16((int)t + 1 - lane);
+                const uint32_t v = pk_mad_i16(jl, MA2, H2[NV - 1]);
+                rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jl, rowbest_j);
                 rowbest = pk_max(rowbest, v);
             }
             if (has_next && (uint32_t)lane == nl - 1) io.B[j] = (int32_t)(UZ ? pk_sub(H2[R - 1], rep16(dl * lane)) : H2[R - 1]);
