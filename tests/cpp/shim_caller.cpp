@@ -4,7 +4,8 @@
 // (CMakeLists.txt:32-36).  Reads cases "type match mismatch gap qhex thex"
 // from stdin; prints "score tb cigarhex" or "ERR <what()>" per case, like the
 // mapper's try/catch at team_mapper.cpp:663-683.  With argv[1] == "threads"
-// the cases are run from 4 threads at once (the mapper's OpenMP loop).
+// the cases are run from argv[2] (default 4) threads at once (the mapper's
+// OpenMP loop).
 #include <cstdio>
 #include <iostream>
 #include <sstream>
@@ -66,10 +67,11 @@ int main(int argc, char** argv) {
         cases.push_back(c);
     }
     if (argc > 1 && std::string(argv[1]) == "threads") {
+        const int T = argc > 2 ? std::stoi(argv[2]) : 4;  // concurrent calls are combined into batches
         std::vector<std::thread> th;
-        for (int w = 0; w < 4; ++w)
-            th.emplace_back([&, w] {
-                for (size_t i = w; i < cases.size(); i += 4) run(cases[i]);
+        for (int w = 0; w < T; ++w)
+            th.emplace_back([&, w, T] {
+                for (size_t i = w; i < cases.size(); i += (size_t)T) run(cases[i]);
             });
         for (auto& t : th) t.join();
     } else {

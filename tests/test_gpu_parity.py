@@ -196,7 +196,7 @@ def test_team_align_dropin(kat_cases, random_cases):
     """An unmodified team::Align caller links and gets the reference's
     answers (incl. the exception message), single- and multi-threaded."""
     exe = _shim_binary()
-    cases = kat_cases + random_cases[:60]
+    cases = kat_cases + random_cases
     lines = [f"{c['type']} {c['match']} {c['mismatch']} {c['gap']} {c['query'] or '-'} {c['target'] or '-'}"
              for c in cases]
     want = []
@@ -205,7 +205,7 @@ def test_team_align_dropin(kat_cases, random_cases):
             want.append(f"ERR {c['error']}")
         else:
             want.append(f"{c['score']} {c['target_begin']} {c['cigar'] or '-'}")
-    for mode in ([], ["threads"]):
+    for mode in ([], ["threads"], ["threads", "16"]):  # combined batches of mixed scorings and errors
         out = subprocess.run([exe] + mode, input="\n".join(lines) + "\n", capture_output=True, text=True,
                              timeout=600, check=True).stdout.splitlines()
         assert out == want
