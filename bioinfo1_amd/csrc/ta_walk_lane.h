@@ -51,7 +51,10 @@ __device__ __forceinline__ uint32_t lds_ld16(uint32_t a) { return *(const lds_u1
 __device__ __forceinline__ void lds_st32(uint32_t a, uint32_t v) { *(lds_u32*)(uintptr_t)a = v; }
 
 constexpr int kLwStripes = 8;                          // tile rows: 8 stripes = 128 query rows
-constexpr int kLwSteps = 64;                           // tile columns: 64 steps of the pass
+#ifndef TA_LW_STEPS
+#define TA_LW_STEPS 64
+#endif
+constexpr int kLwSteps = TA_LW_STEPS;                  // tile columns: 64 steps of the pass
 constexpr int kLwRunCap = 64;                          // runs listed before a flush
 constexpr int kLwTileDw = kLwStripes * kLwSteps;       // 512 dwords
 constexpr int kLwQEnt = kLwStripes * kRows;            // 128 query rows (u16: byte | indel cost << 8)
