@@ -77,8 +77,8 @@ struct LwStage {
 // the last one (the walk only moves up and left), and set the tile
 // coordinates of the cell: lr = row - rowbase in [0, 128), lc = col - cb in
 // [0, 71], its step lc + (lr >> 4) - 7.  Every load comes from a clamped
-// (valid) address and is masked in lw_commit, so a stage costs one memory
-// latency.  All G lanes of the group.
+// (valid) address, so a stage costs one memory latency.  All G lanes of the
+// group.
 template <int G>
 __device__ __forceinline__ void lw_issue(int row, int col, int& rowbase, int& cb, int& lr, int& lc, uint32_t& T0,
                                          LwStage<G>& st, const uint32_t* P, const uint8_t* Q, const uint8_t* T,
@@ -92,11 +92,12 @@ __device__ __forceinline__ void lw_issue(int row, int col, int& rowbase, int& cb
     cb = (int)T0 - (int)L0 - (kLwStripes - 1);
     lr = row - rowbase;
     lc = col - cb;
-    const uint64_t pass_base = (uint64_t)tP * Tmax;
+    // one 64-bit base per stage, 32-bit dword offsets per load (full-rate math)
+    const uint32_t* Pp = P + ((uint64_t)tP * Tmax * kWave + L0);
 #pragma unroll
     for (int k = 0; k < LwStage<G>::NL; ++k) {
         const uint32_t x = li + (uint32_t)G * k, ts = min(T0 + (x >> 1), Tmax - 1u);
-        st.v[k] = *(const uint4*)(P + (pass_base + ts) * kWave + L0 + 4u * (x & 1u));
+        st.v[k] = *(const uint4*)(Pp + (ts * (uint32_t)kWave + 4u * (x & 1u)));
     }
 #pragma unroll
     for (int k = 0; k < LwStage<G>::NQ; ++k) st.q[k] = Q[min((uint32_t)rowbase + li + (uint32_t)G * k, n - 1u)];
@@ -106,29 +107,23 @@ __device__ __forceinline__ void lw_issue(int row, int col, int& rowbase, int& cb
 }
 
 // Write a staged tile into the group's LDS: codes ([step][stripe] dwords),
-// query rows and target columns as u16 (byte | indel cost << 8; 0 outside the
-// sequences, never read).
+// query rows and target columns as u16 (byte | indel cost << 8).  Entries
+// outside the pass or the sequences hold copies of clamped in-range loads: the
+// walk reads only the cells of its path, which lie inside both.
 template <int G>
-__device__ __forceinline__ void lw_commit(const LwStage<G>& st, int rowbase, int cb, uint32_t T0, uint32_t* tile,
-                                          uint16_t* qw, uint16_t* tw, uint32_t n, uint32_t m, int gap, uint32_t li) {
-    const uint32_t Tmax = pass_steps(m);
+__device__ __forceinline__ void lw_commit(const LwStage<G>& st, uint32_t* tile, uint16_t* qw, uint16_t* tw, int gap,
+                                          uint32_t li) {
     const uint32_t gq = (uint32_t)gap & 0xFFu;
 #pragma unroll
-    for (int k = 0; k < LwStage<G>::NL; ++k) {
-        const uint32_t x = li + (uint32_t)G * k;
-        *(uint4*)(tile + 4u * x) = (T0 + (x >> 1) < Tmax) ? st.v[k] : make_uint4(0u, 0u, 0u, 0u);
-    }
+    for (int k = 0; k < LwStage<G>::NL; ++k) *(uint4*)(tile + 4u * (li + (uint32_t)G * k)) = st.v[k];
 #pragma unroll
     for (int k = 0; k < LwStage<G>::NQ; ++k) {
-        const uint32_t e = li + (uint32_t)G * k;
-        const uint32_t c = (uint32_t)rowbase + e < n ? st.q[k] : 0u;
-        qw[e] = (uint16_t)(c | ((c == '-' ? 0u : gq) << 8));
+        const uint32_t c = st.q[k];
+        qw[li + (uint32_t)G * k] = (uint16_t)(c | ((c == '-' ? 0u : gq) << 8));
     }
 #pragma unroll
     for (int k = 0; k < LwStage<G>::NT; ++k) {
-        const uint32_t e = li + (uint32_t)G * k;
-        const int cc = cb + (int)e;
-        const uint32_t c = (cc >= 0 && (uint32_t)cc < m) ? st.t[k] : 0u;
+        const uint32_t e = li + (uint32_t)G * k, c = st.t[k];
         if (e < (uint32_t)kLwTEnt) tw[e] = (uint16_t)(c | ((c == '-' ? 0u : gq) << 8));
     }
 }
@@ -231,7 +226,7 @@ __device__ __forceinline__ void traceback_lane_local(const TraceArgs& a, uint32_
                     live = false;  // (cannot happen: the cost of row / column 0 is 0)
                 } else {
                     lw_issue<G>(row, col, rowbase, cb, lr, lc, T0, st, P, Q, T, n, m, li);
-                    lw_commit<G>(st, rowbase, cb, T0, tile, qw, tw, n, m, gap, li);
+                    lw_commit<G>(st, tile, qw, tw, gap, li);
                 }
                 stage = false;
             }
