@@ -55,7 +55,10 @@ constexpr int kLwStripes = 8;                          // tile rows: 8 stripes =
 #define TA_LW_STEPS 64
 #endif
 constexpr int kLwSteps = TA_LW_STEPS;                  // tile columns: 64 steps of the pass
-constexpr int kLwRunCap = 64;                          // runs listed before a flush
+#ifndef TA_LW_RUNS
+#define TA_LW_RUNS 64
+#endif
+constexpr int kLwRunCap = TA_LW_RUNS;                  // runs listed before a flush
 constexpr int kLwTileDw = kLwStripes * kLwSteps;       // 512 dwords
 constexpr int kLwQEnt = kLwStripes * kRows;            // 128 query rows (u16: byte | indel cost << 8)
 constexpr int kLwTEnt = kLwSteps + kLwStripes;         // 72 target columns (u16 likewise)
