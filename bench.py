@@ -189,18 +189,34 @@ class Dist:
 
 
 class ResultGather:
-    """Every step's results of every rank gathered to every rank (all_gather;
-    rank 0 is the consumer).  Records of step k: one all_gather right after its
-    kernels.  CIGAR bytes of step k (compacted on the device, ta_compact_cigars):
-    posted once step k+1 is enqueued -- their sizes ride in step k's records,
-    which by then have arrived without stalling the GPU -- padded to the largest
-    rank's byte count (RCCL has no gatherv)."""
+    """Every step's results of every rank gathered to rank 0, the only consumer
+    (SURVEY §8e); the other ranks receive nothing.
+
+    Records of step k (score, target_begin, cigar_len per pair, plus the pair
+    and CIGAR-byte counts): one ``gather`` to rank 0 right after the step's
+    kernels.  CIGAR bytes of step k (compacted on the device,
+    ta_compact_cigars): point-to-point, exactly each rank's byte count (RCCL
+    has no gatherv; rank 0 learns the counts from step k's records), posted
+    once step k+1 is enqueued, so neither stalls the GPU.  With RCCL every
+    transfer runs on a side stream that waits only for the event recorded
+    after step k's compaction: the compute stream never waits for a gather,
+    and a send never waits for step k+1's kernels.  All transfers are drained
+    before the clock stops."""
 
     def __init__(self, D: Dist, P_max: int, cigar: bool):
         import torch
 
         self.torch, self.D, self.P, self.cigar = torch, D, P_max, cigar
+        self.root = D.rank == 0
+        self.nccl = D.backend == "nccl"
+        self.side = torch.cuda.Stream(D.dev) if self.nccl else None
         self.pending = []
+        self.recv_bytes = 0  # bytes this rank received over all steps (0 on ranks > 0)
+
+    def _ctx(self):
+        import contextlib
+
+        return self.torch.cuda.stream(self.side) if self.nccl else contextlib.nullcontext()
 
     def post(self, plan):
         torch, D, P = self.torch, self.D, self.P
@@ -214,77 +230,116 @@ class ResultGather:
             dst, off = plan.compact_cigars()
             rec[3 * P + 1] = off[-1].to(torch.int32)
         rec[3 * P] = n
-        st = {"dst": dst}
-        if D.backend == "nccl":
-            out = torch.empty(D.world * rec.numel(), dtype=torch.int32, device=D.dev)
-            st["h"] = D.all_gather_flat(out, rec, True)
-            st["h"].wait()  # the current stream waits for the gather; the host does not
-            tot = torch.empty((D.world, 2), dtype=torch.int32, pin_memory=True)
-            tot.copy_(out.view(D.world, -1)[:, 3 * P:], non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record()
-            st.update(out=out, tot=tot, ev=ev)
+        st = {"dst": dst, "works": []}
+        if self.nccl:
+            ready = torch.cuda.Event()
+            ready.record()  # step k's records and compacted bytes, on the compute stream
+            st["ready"] = ready
+            with self._ctx():
+                self.side.wait_event(ready)
+                # this rank's own pair / byte counts, to the host without waiting for step k+1
+                cnt = torch.empty(2, dtype=torch.int32, pin_memory=True)
+                cnt.copy_(rec[3 * P:], non_blocking=True)
+                cev = torch.cuda.Event()
+                cev.record()
+                st.update(cnt=cnt, cev=cev)
+                outs = [torch.empty_like(rec) for _ in range(D.world)] if self.root else None
+                st["works"].append(D.dist.gather(rec, outs, dst=0, async_op=True))
+                if self.root:
+                    st["works"][-1].wait()  # the side stream waits, not the compute stream
+                    tot = torch.empty((D.world, 2), dtype=torch.int32, pin_memory=True)
+                    tot.copy_(torch.stack([o[3 * P:] for o in outs]), non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record()
+                    st.update(outs=outs, tot=tot, ev=ev)
+            st["rec"] = rec
         else:
-            out = torch.empty(D.world * rec.numel(), dtype=torch.int32)
-            D.all_gather_flat(out, rec.cpu(), False)
-            st.update(out=out, tot=out.view(D.world, -1)[:, 3 * P:].clone(), ev=None)
+            rec_h = rec.cpu()
+            st.update(cnt=rec_h[3 * P:].clone(), cev=None)
+            outs = [torch.empty_like(rec_h) for _ in range(D.world)] if self.root else None
+            D.dist.gather(rec_h, outs, dst=0)
+            if self.root:
+                st.update(outs=outs, tot=torch.stack([o[3 * P:] for o in outs]), ev=None)
+        if self.root:
+            self.recv_bytes += (D.world - 1) * rec.numel() * 4
         if self.cigar and self.pending and "bytes" not in self.pending[-1]:
             self._post_bytes(self.pending[-1])
         self.pending.append(st)
 
     def _post_bytes(self, st):
         torch, D = self.torch, self.D
-        if st["ev"] is not None:
-            st["ev"].synchronize()  # step k's records are in: the GPU is already busy with step k+1
-        tot = st["tot"][:, 1].numpy()
-        words = max(1, (int(tot.max()) + 3) // 4)
+        dev = D.dev if self.nccl else torch.device("cpu")
         dst = st["dst"]
-        if dst.numel() < 4 * words:
-            buf = torch.zeros(4 * words, dtype=torch.uint8, device=dst.device)
-            buf[:dst.numel()] = dst
-            dst = buf
-        mine = dst[:4 * words].view(torch.int32)
-        if D.backend == "nccl":
-            out = torch.empty(D.world * words, dtype=torch.int32, device=D.dev)
-            st["h2"] = D.all_gather_flat(out, mine, True)
+        if self.root:
+            if st["ev"] is not None:
+                st["ev"].synchronize()  # step k's records are in: the GPU is already busy with step k+1
+            nbytes = [int(x) for x in st["tot"][:, 1].tolist()]
         else:
-            out = torch.empty(D.world * words, dtype=torch.int32)
-            D.all_gather_flat(out, mine.cpu(), False)
-            st["h2"] = None
-        st["bytes"] = (out, words)
+            nbytes = None
+        with self._ctx():
+            if self.root:
+                mine = dst[:nbytes[0]] if nbytes[0] else dst[:0]
+                bufs = [mine if self.nccl else mine.cpu()]
+                ops = []
+                for r in range(1, D.world):
+                    words = (nbytes[r] + 3) // 4
+                    b = torch.empty(words, dtype=torch.int32, device=dev)
+                    bufs.append(b)
+                    if words:
+                        ops.append(D.dist.P2POp(D.dist.irecv, b, r))
+                    self.recv_bytes += 4 * words
+                st["bufs"] = bufs
+                st["nbytes"] = nbytes
+            else:
+                # this rank's byte count (its records' last word); whole int32 words go (rank 0 drops the slack)
+                if st["cev"] is not None:
+                    st["cev"].synchronize()  # step k's count only: the GPU is already busy with step k+1
+                words = (int(st["cnt"][1]) + 3) // 4
+                ops = []
+                if words:
+                    w = dst[:4 * words].view(torch.int32) if self.nccl else dst[:4 * words].cpu().view(torch.int32)
+                    st["send"] = w
+                    ops.append(D.dist.P2POp(D.dist.isend, w, 0))
+            if ops:
+                st["works"] += D.dist.batch_isend_irecv(ops)
+        st["bytes"] = True
 
     def drain(self):
         for st in self.pending:
             if self.cigar and "bytes" not in st:
                 self._post_bytes(st)
-        for st in self.pending:
-            for h in (st.get("h"), st.get("h2")):
-                if h is not None:
-                    h.wait()
+        with self._ctx():  # RCCL: the side stream waits for the transfers, then the compute stream for it
+            for st in self.pending:
+                for w in st["works"]:
+                    w.wait()
+        if self.nccl:
+            self.torch.cuda.current_stream(self.D.dev).wait_stream(self.side)
 
     def last(self):
-        """Rank-ordered (scores, target_begins, cigar_lens, cigar bytes) of the last step."""
+        """Rank 0: rank-ordered (scores, target_begins, cigar_lens, cigar bytes) of the last step."""
+        assert self.root, "results are gathered to rank 0 only"
         st = self.pending[-1]
         P, W = self.P, self.D.world
-        rec = st["out"].view(W, -1).cpu().numpy()
+        rec = self.torch.stack(st["outs"]).cpu().numpy()
         n = rec[:, 3 * P]
         sc = np.concatenate([rec[r, :n[r]] for r in range(W)])
         tb = np.concatenate([rec[r, P:P + n[r]] for r in range(W)]).view(np.uint32)
         cl = np.concatenate([rec[r, 2 * P:2 * P + n[r]] for r in range(W)]).view(np.uint32)
         cig = None
         if self.cigar:
-            out, words = st["bytes"]
-            by = out.view(W, words).cpu().numpy().view(np.uint8)
-            cig = b"".join(by[r, :rec[r, 3 * P + 1]].tobytes() for r in range(W))
+            parts = []
+            for r, b in enumerate(st["bufs"]):
+                parts.append(b.cpu().numpy().view(np.uint8)[:st["nbytes"][r]].tobytes())
+            cig = b"".join(parts)
         return sc, tb, cl, cig
 
     def clear_old(self, keep=2):
-        # finished steps (their byte gathers posted) can go; waits keep the allocator safe
+        # finished steps (their byte transfers posted) can go; waits keep the allocator safe
         while len(self.pending) > keep and "bytes" in self.pending[0]:
             st = self.pending.pop(0)
-            for h in (st.get("h"), st.get("h2")):
-                if h is not None:
-                    h.wait()
+            with self._ctx():
+                for w in st["works"]:
+                    w.wait()
 
 
 # --------------------------------------------------------------------------- inputs
@@ -414,6 +469,51 @@ def parity_vs_digest(scores, tbs, clens, cigar_of, name, k):
     return {"golden": f"tests/golden/digest_{name}", "pairs_checked": k, "bit_exact": ok}
 
 
+def strided_name(args):
+    """The stratified reference digest (pairs spread over the whole stated-size
+    stream, tests/golden/make_golden.py) that covers this workload, or None."""
+    if args.gap_open is not None or args.scoring != "1,-1,-1":
+        return None
+    if args.workload == "cfg5" and args.mode == "semiGlobal" and (args.qlen, args.tlen) == (10000, 10000):
+        return "cfg5_semi_strided"
+    if args.workload in ("cfg3", "cfg4"):
+        return {"semiGlobal": "cfg3_semi_strided", "local": "cfg3_local_strided"}.get(args.mode)
+    return None
+
+
+def parity_strided(scores, tbs, clens, cigar_of, name, lo, hi, chunk_of=None, n_chunks=None):
+    """The pairs of the stratified digest `name` that fall in this run's stream
+    range [lo, hi) (pair p of the run is stream position lo + p), each against
+    the reference's score, target_begin, CIGAR length and CIGAR CRC32; with all
+    of them present also the SHA-256 over the whole sample.  chunk_of (per
+    pair) shows which chunks of the plan the checked pairs ran in."""
+    import zlib
+
+    with open(os.path.join(ROOT, "tests", "golden", f"digest_{name}.json")) as f:
+        meta = json.load(f)
+    d = np.load(os.path.join(ROOT, "tests", "golden", f"digest_{name}.npz"))
+    idx = d["indices"]
+    sel = np.nonzero((idx >= lo) & (idx < hi))[0]
+    loc = (idx[sel] - lo).astype(np.int64)
+    cig = [cigar_of(int(p)) for p in loc]
+    ok = bool(np.array_equal(scores[loc], d["scores"][sel]) and np.array_equal(tbs[loc], d["target_begins"][sel])
+              and np.array_equal(clens[loc], d["cigar_lens"][sel])
+              and all(zlib.crc32(c) == int(d["cigar_crc32"][k]) for c, k in zip(cig, sel)))
+    if len(sel) == len(idx):
+        h = hashlib.sha256()
+        for c in cig:
+            h.update(len(c).to_bytes(4, "little"))
+            h.update(c)
+        ok = ok and h.hexdigest() == meta["cigar_sha256"]
+    out = {"golden": f"tests/golden/digest_{name}", "pairs_checked": int(len(sel)), "sample_size": int(len(idx)),
+           "stream_positions": f"{int(idx[sel].min()) if len(sel) else '-'}..{int(idx[sel].max()) if len(sel) else '-'}",
+           "bit_exact": ok}
+    if chunk_of is not None and len(sel):
+        out["chunks_covered"] = int(len(np.unique(chunk_of[loc])))
+        out["chunks"] = int(n_chunks)
+    return out
+
+
 def parity_vs_oracle(res, batch, mode, sc, gap_open, k):
     """Affine extension (no reference digest exists for gap_open != 0): the
     first k pairs against the CPU definition (oracle/affine_oracle.c)."""
@@ -514,6 +614,12 @@ def main_align(args, D):
         name, k = digest_name(args, plan.P)
         if name and cigar and not affine and lo == 0:
             parity = parity_vs_digest(res.scores, res.target_begins, res.cigar_lens, res.cigar, name, k)
+            sname = strided_name(args)
+            if sname:
+                parity["digest_stratified"] = parity_strided(res.scores, res.target_begins, res.cigar_lens,
+                                                             res.cigar, sname, lo, hi, plan.pair_chunks(),
+                                                             plan.chunks)
+                parity["bit_exact"] = parity["bit_exact"] and parity["digest_stratified"]["bit_exact"]
         elif affine and cigar:
             parity = parity_vs_oracle(res, host_batch_of(batch, dev_in, 16), mode, sc, args.gap_open, 16)
     D.barrier()
@@ -650,6 +756,11 @@ def check_gathered(args, gathered, plan, full, al, mode, sc, cigar):
             d = parity_vs_digest(sc_g, tb_g, cl_g, lambda p: cig_g[offs[p]:offs[p + 1]], name, k)
             res["digest"] = d
             res["bit_exact"] = res["bit_exact"] and d["bit_exact"]
+            sname = strided_name(args)
+            if sname:
+                ds = parity_strided(sc_g, tb_g, cl_g, lambda p: cig_g[offs[p]:offs[p + 1]], sname, 0, full.n_pairs)
+                res["digest_stratified"] = ds
+                res["bit_exact"] = res["bit_exact"] and ds["bit_exact"]
         return res
     r = plan.results()
     n = plan.P

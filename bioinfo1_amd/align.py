@@ -92,6 +92,8 @@ def lib() -> C.CDLL:
     L.ta_plan_flex_pairs.restype = C.c_uint32
     L.ta_plan_flex_pairs.argtypes = [C.c_void_p]
     L.ta_plan_fused.argtypes = [C.c_void_p]
+    L.ta_plan_pair_chunks.argtypes = [C.c_void_p, u32p]
+    L.ta_affine_plan_pair_chunks.argtypes = [C.c_void_p, u32p]
     L.ta_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ta_plan_check.argtypes = [C.c_void_p]
     L.ta_compact_cigars.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p,
@@ -126,7 +128,7 @@ ABI_SYMBOLS = [
     "ta_context_held_bytes",
     "ta_cigar_slot_bytes", "ta_align_batch", "ta_align_batch_flags", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes",
     "ta_plan_workspace_bytes", "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_fused",
-    "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_execute_traceback", "ta_compact_cigars",
+    "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_pair_chunks", "ta_affine_plan_pair_chunks", "ta_plan_execute_traceback", "ta_compact_cigars",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
     "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
@@ -390,6 +392,35 @@ class DevicePlan:
         if r != TA_OK:
             _raise(r, self._ctx)
         return dst, off
+
+    def pair_chunks(self) -> np.ndarray:
+        """uint32 [P]: the chunk each pair ran in (ta_plan_pair_chunks)."""
+        out = np.zeros(max(self.P, 1), np.uint32)
+        r = self._fn("ta_plan_pair_chunks")(self._h, _p(out, C.c_uint32))
+        if r != TA_OK:
+            _raise(r, self._ctx)
+        return out[: self.P]
+
+    def results_at(self, indices) -> BatchResult:
+        """Synchronise, check and copy the results of the pairs ``indices`` only
+        (the stratified parity checks of a stated-size run): a BatchResult whose
+        k-th entry is pair indices[k]."""
+        torch = self.torch
+        self.check()
+        idx = torch.as_tensor(np.asarray(indices, np.int64), device=self.dev)
+        sc = self.score[idx].cpu().numpy()
+        tb = self.target_begin[idx].cpu().numpy().view(np.uint32)
+        if not self.want_cigar:
+            return BatchResult(sc, tb, None, None, None)
+        start = self.cigar_start[idx].cpu().numpy()
+        ln = self.cigar_len[idx].cpu().numpy().view(np.uint32)
+        parts, offs, o = [], np.zeros(len(ln), np.uint64), 0
+        for k in range(len(ln)):
+            parts.append(self.slots[int(start[k]):int(start[k]) + int(ln[k])].cpu().numpy())
+            offs[k] = o
+            o += int(ln[k])
+        arena = np.concatenate(parts) if parts else np.zeros(1, np.uint8)
+        return BatchResult(sc, tb, offs, ln, arena)
 
     def results(self) -> BatchResult:
         """Synchronise, check and copy results to host (CIGARs unpacked from slots)."""

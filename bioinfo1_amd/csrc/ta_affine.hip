@@ -744,9 +744,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     const bool cls = __ballot(qother) == 0;
     if (__ballot(qdash)) {  // per-row vertical gap constants: the int32 fill takes the couple
         if (lane == 0) {
-            const uint32_t at = atomicAdd(a.fb_count, 2u);
+            // a self-coupled pair (p[0] == p[1], ta_planner.cpp) is handed back once:
+            // two int32 waves on one pair would share its in-place boundary row
+            const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
+            const uint32_t at = atomicAdd(a.fb_count, k);
             a.fb_list[at] = p[0];
-            a.fb_list[at + 1] = p[1];
+            if (k == 2) a.fb_list[at + 1] = p[1];
         }
         return;
     }
@@ -1090,6 +1093,15 @@ uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* pl) {
 }
 uint32_t ta_affine_plan_chunks(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->h.chunks.size() : 0; }
 uint32_t ta_affine_plan_dual_pairs(const ta_affine_plan* pl) { return pl ? (uint32_t)pl->h.duals.size() : 0; }
+
+int ta_affine_plan_pair_chunks(const ta_affine_plan* pl, uint32_t* chunk_of_pair) {
+    if (!pl || !chunk_of_pair) return TA_ERR_ARG;
+    for (uint32_t c = 0; c < (uint32_t)pl->h.chunks.size(); ++c) {
+        const auto& ch = pl->h.chunks[c];
+        for (uint32_t k = ch.begin; k < ch.begin + ch.count; ++k) chunk_of_pair[pl->h.order[k]] = c;
+    }
+    return TA_OK;
+}
 
 int ta_affine_plan_execute(ta_affine_plan* pl, const ta_device_io* io, void* stream) {
     if (int r = affine_check_io(pl, io)) return r;

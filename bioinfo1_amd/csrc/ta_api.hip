@@ -425,6 +425,15 @@ uint32_t ta_plan_dual_pairs(const ta_plan* pl) { return pl ? pl->h.n_dual_pairs 
 uint32_t ta_plan_flex_pairs(const ta_plan* pl) { return pl ? (uint32_t)pl->h.flexes.size() : 0; }
 int ta_plan_fused(const ta_plan* pl) { return pl && pl->h.fused ? 1 : 0; }
 
+int ta_plan_pair_chunks(const ta_plan* pl, uint32_t* chunk_of_pair) {
+    if (!pl || !chunk_of_pair) return TA_ERR_ARG;
+    for (uint32_t c = 0; c < (uint32_t)pl->h.chunks.size(); ++c) {
+        const auto& ch = pl->h.chunks[c];
+        for (uint32_t k = ch.begin; k < ch.begin + ch.count; ++k) chunk_of_pair[pl->h.order[k]] = c;
+    }
+    return TA_OK;
+}
+
 int ta_plan_execute(ta_plan* pl, const ta_device_io* io, void* stream) {
     if (int r = check_io(pl, io)) return r;
     std::lock_guard<std::mutex> lock(pl->ctx->mu);

@@ -385,9 +385,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     // same workspace).
     if (__ballot(dash)) {
         if (lane == 0) {
-            const uint32_t at = atomicAdd(a.fb_count, 2u);
+            // a self-coupled pair (p[0] == p[1], ta_planner.cpp) is handed back once:
+            // two int32 waves on one pair would share its in-place boundary row
+            const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
+            const uint32_t at = atomicAdd(a.fb_count, k);
             a.fb_list[at] = p[0];
-            a.fb_list[at + 1] = p[1];
+            if (k == 2) a.fb_list[at + 1] = p[1];
         }
         return;
     }

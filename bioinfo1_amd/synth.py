@@ -237,6 +237,13 @@ def related_batch_torch(n_pairs: int, qlen: int, tlen: int, seed: int = 0x5EED, 
     return Q, T
 
 
+def related_pairs_at(indices, qlen: int, tlen: int, seed: int = 0x5EED, rate: float = 0.05) -> PairBatch:
+    """The pairs at stream positions ``indices`` of related_batch's stream (pair p
+    depends only on ``seed ^ p``): the stratified samples of config 5's 100k-pair
+    stream that the golden digests pin (tests/golden/make_golden.py)."""
+    return _concat([related_batch(1, qlen, tlen, seed, rate, first_pair=int(p)) for p in indices])
+
+
 def ragged_batch(n_pairs: int, min_len: int, max_len: int, seed: int = 0x5EED, alphabet: bytes = b"ACGT",
                  first_pair: int = 0) -> PairBatch:
     """Independent random lengths in [min_len, max_len] for query and target,
@@ -313,16 +320,21 @@ def _mutate(seg: np.ndarray, d: np.ndarray, rate: float) -> np.ndarray:
 
 
 def ont_reads(n_reads: int, ref: np.ndarray, seed: int = 0x0E7, median: float = 9000.0, sigma: float = 0.5,
-              min_len: int = 1000, max_len: int = 20000, error: float = 0.10, first_read: int = 0) -> ReadSet:
+              min_len: int = 1000, max_len: int = 20000, error: float = 0.10, first_read: int = 0,
+              indices=None) -> ReadSet:
     """ONT-like reads: log-normal segment lengths (median ``median``, clamped to
     [min_len, max_len]), uniform start, 50 % reverse-complement strand, then
     ``error`` total substitution/insertion/deletion rate (a third each).
     Read r's stream starts from state ``seed ^ r``: 4 header draws (two for the
-    length, start, strand), then 2 draws per segment base."""
+    length, start, strand), then 2 draws per segment base.  ``indices``: the
+    reads at these stream positions instead of ``first_read ..`` (each read is
+    independent of the others, so read r is the same bytes in any set)."""
     G = int(ref.shape[0])
     max_len = min(max_len, G)
     chunks, lens, starts, segs, revs = [], [], [], [], []
-    for r in range(first_read, first_read + n_reads):
+    idx = range(first_read, first_read + n_reads) if indices is None else [int(r) for r in indices]
+    n_reads = len(idx)
+    for r in idx:
         st = np.uint64(seed) ^ np.uint64(r)
         h = stream(st, 0, 4)
         u1 = (float(h[0] >> np.uint64(11)) + 1.0) * (1.0 / 2**53)
@@ -369,9 +381,17 @@ def origin_batch(reads: ReadSet, ref: np.ndarray) -> PairBatch:
 ECOLI_LEN = 4_641_652  # NC_000913.3
 
 
-def cfg3_batch(n_reads: int = 10000, first_read: int = 0, genome_seed: int = 0xEC011, read_seed: int = 0x0E7):
+def cfg3_batch(n_reads: int = 10000, first_read: int = 0, genome_seed: int = 0xEC011, read_seed: int = 0x0E7,
+               indices=None):
     """Config 3 stand-in: reads of a 4.64 Mb i.i.d. genome against
-    their true-origin windows.  Returns (PairBatch, ReadSet, genome)."""
+    their true-origin windows.  Returns (PairBatch, ReadSet, genome).
+    ``indices``: only the reads at these positions of the read stream."""
     g = genome(ECOLI_LEN, genome_seed)
-    rs = ont_reads(n_reads, g, read_seed, first_read=first_read)
+    rs = ont_reads(n_reads, g, read_seed, first_read=first_read, indices=indices)
     return origin_batch(rs, g), rs, g
+
+
+# stratified digest positions (tests/golden/make_golden.py): pairs from every chunk of the
+# stated-size runs, not only the first ones
+CFG5_STRIDED = np.arange(128, dtype=np.int64) * 781   # 0 .. 99,187 of config 5's 100,000 pairs
+CFG3_STRIDED = np.arange(256, dtype=np.int64) * 39    # 0 .. 9,945 of config 3's 10,000 reads

@@ -13,32 +13,43 @@ B="$ROOT/build"
 mkdir -p "$B"
 FLAGS=(-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-unused-function ${TA_EXTRA_FLAGS:-})
 pids=()
+# incremental: an object is rebuilt when its source or any csrc header is newer (TA_FORCE=1: always)
+if [ "$(cat "$B/.flags" 2>/dev/null)" != "${FLAGS[*]}" ]; then TA_FORCE=1; fi  # other flags: rebuild all
+echo "${FLAGS[*]}" > "$B/.flags"
+HNEW=$(ls -t "$CS"/*.h "$ROOT"/include/*.h* 2>/dev/null | sed -n 1p)
+stale() {  # stale <obj> <src>
+  [ "${TA_FORCE:-0}" = 1 ] || [ ! -f "$1" ] || [ "$2" -nt "$1" ] || [ "$HNEW" -nt "$1" ] || [ "$0" -nt "$1" ]
+}
+cc() {  # cc <obj> <src> <compiler args...>: background compile when stale
+  local o="$1" src="$2"; shift 2
+  if stale "$o" "$src"; then "$@" -o "$o" & pids+=($!); fi
+}
 for m in 0 1 2; do
   for c in 0 1; do
-    "$HIPCC" "${FLAGS[@]}" -DTA_FILL_MODE=$m -DTA_FILL_CIGAR=$c -c "$CS/ta_kernels.hip" -o "$B/ta_fill_$m$c.o" & pids+=($!)
-    "$HIPCC" "${FLAGS[@]}" -DTA_DUAL_MODE=$m -DTA_DUAL_CIGAR=$c -c "$CS/ta_dual.hip" -o "$B/ta_dual_$m$c.o" & pids+=($!)
+    cc "$B/ta_fill_$m$c.o" "$CS/ta_kernels.hip" "$HIPCC" "${FLAGS[@]}" -DTA_FILL_MODE=$m -DTA_FILL_CIGAR=$c -c "$CS/ta_kernels.hip"
+    cc "$B/ta_dual_$m$c.o" "$CS/ta_dual.hip" "$HIPCC" "${FLAGS[@]}" -DTA_DUAL_MODE=$m -DTA_DUAL_CIGAR=$c -c "$CS/ta_dual.hip"
   done
 done
 for m in 0 1 2; do
   for c in 0 1; do
-    "$HIPCC" "${FLAGS[@]}" -DTA_FLEX_MODE=$m -DTA_FLEX_CIGAR=$c -c "$CS/ta_flex.hip" -o "$B/ta_flex_$m$c.o" & pids+=($!)
+    cc "$B/ta_flex_$m$c.o" "$CS/ta_flex.hip" "$HIPCC" "${FLAGS[@]}" -DTA_FLEX_MODE=$m -DTA_FLEX_CIGAR=$c -c "$CS/ta_flex.hip"
   done
 done
-"$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$CS/ta_kernels.hip" -o "$B/ta_misc.o" & pids+=($!)
+cc "$B/ta_misc.o" "$CS/ta_kernels.hip" "$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$CS/ta_kernels.hip"
 # affine-gap extension (fill + traceback kernels and its plan driver)
-"$HIPCC" "${FLAGS[@]}" -c "$CS/ta_affine.hip" -o "$B/ta_affine.o" & pids+=($!)
-"$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip" -o "$B/ta_api.o" & pids+=($!)
-"$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp" -o "$B/shim.o" & pids+=($!)
+cc "$B/ta_affine.o" "$CS/ta_affine.hip" "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_affine.hip"
+cc "$B/ta_api.o" "$CS/ta_api.hip" "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip"
+cc "$B/shim.o" "$CS/team_alignment_shim.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp"
 # host planner: plain C++ (also built with g++ under ASan/UBSan/TSan by tests/test_host_sanitizers.py)
-g++ -O2 -std=c++17 -fPIC -Wall -c "$CS/ta_planner.cpp" -o "$B/ta_planner.o" & pids+=($!)
+cc "$B/ta_planner.o" "$CS/ta_planner.cpp" g++ -O2 -std=c++17 -fPIC -Wall -c "$CS/ta_planner.cpp"
 # mapper stages (libteam_mapper.so) and the team_mapper_amd CLI
 for f in tm_minimizers tm_match tm_chain; do
-  "$HIPCC" "${FLAGS[@]}" -c "$CS/$f.hip" -o "$B/$f.o" & pids+=($!)
+  cc "$B/$f.o" "$CS/$f.hip" "$HIPCC" "${FLAGS[@]}" -c "$CS/$f.hip"
 done
 for f in tm_api tm_fastx; do
-  "$HIPCC" "${FLAGS[@]}" -x hip -c "$CS/$f.cpp" -o "$B/$f.o" & pids+=($!)
+  cc "$B/$f.o" "$CS/$f.cpp" "$HIPCC" "${FLAGS[@]}" -x hip -c "$CS/$f.cpp"
 done
-"$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp" -o "$B/tm_main.o" & pids+=($!)
+cc "$B/tm_main.o" "$CS/tm_main.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp"
 for p in "${pids[@]}"; do wait "$p"; done
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_planner.o" "$B/shim.o" \
   -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$OUT"

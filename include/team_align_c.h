@@ -134,6 +134,9 @@ uint32_t ta_plan_dual_pairs(const ta_plan* plan);
 uint32_t ta_plan_flex_pairs(const ta_plan* plan);
 /* 1 when the fill kernel walks its own pair (int32-only plans with CIGAR on). */
 int ta_plan_fused(const ta_plan* plan);
+/* chunk_of_pair[p] = the chunk (0 .. ta_plan_chunks-1) whose launches align pair p
+ * (caller-allocated, n_pairs entries).  Diagnostics: which chunk a checked pair ran in. */
+int ta_plan_pair_chunks(const ta_plan* plan, uint32_t* chunk_of_pair);
 
 /* Device pointers for one execution of a plan. */
 typedef struct ta_device_io {
@@ -206,6 +209,7 @@ uint32_t ta_affine_plan_chunks(const ta_affine_plan* plan);
 /* Pairs the plan runs in the packed two-pairs-per-wave int16 affine fill
  * (global / semi-global couples of equal shape whose values provably fit). */
 uint32_t ta_affine_plan_dual_pairs(const ta_affine_plan* plan);
+int ta_affine_plan_pair_chunks(const ta_affine_plan* plan, uint32_t* chunk_of_pair);
 /* Enqueue the whole batch / one chunk's fill / one chunk's traceback on hip_stream. */
 int ta_affine_plan_execute(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream);
 int ta_affine_plan_execute_fill(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);

@@ -1,4 +1,4 @@
-// scripts/ubench/valu_rates.hip -- cycles per wave-instruction for the VALU
+// scripts/exp/ubench/valu_rates.hip -- cycles per wave-instruction for the VALU
 // ops the DP kernels use (MI355X).  Each kernel runs 8 independent chains of
 // one op per wave, 8 waves per SIMD, and reports the chip-wide rate.
 // Build + run on the GPU box: hipcc -O3 --offload-arch=gfx950 valu_rates.hip -o vr && ./vr
@@ -34,6 +34,18 @@ OPK(k_addc, "v_addc_co_u32 %0, vcc, %0, %0, vcc")
 OPK(k_bfe, "v_bfe_u32 %0, %0, %1, 2")
 OPK(k_lshl_or, "v_lshl_or_b32 %0, %0, 1, %1")
 OPK(k_pk_fma_f32_probe, "v_pk_add_u16 %0, %0, %1 op_sel_hi:[1,1]")
+// the dual fill's remaining per-cell ops (ta_dual.hip): saturating packed subtract,
+// f16 three-input maximum on int16 bit patterns, bit-field insert, packed mad, DPP hand-off
+OPK(k_pk_sub_i16_clamp, "v_pk_sub_i16 %0, %0, %1 clamp")
+OPK(k_pk_max3_f16, "v_pk_maximum3_f16 %0, %0, %1, %0")
+OPK(k_bfi, "v_bfi_b32 %0, %1, %0, %1")
+OPK(k_pk_mad_u16, "v_pk_mad_u16 %0, %0, %1, %0")
+OPK(k_pk_max_i16_opsel, "v_pk_max_i16 %0, %0, %1 op_sel:[0,1] op_sel_hi:[1,1]")
+OPK(k_mov, "v_mov_b32 %0, %1\n v_add_u32 %0, %0, %1")
+OPK(k_dpp_shr, "v_mov_b32_dpp %0, %0 wave_shr:1 row_mask:0xf bank_mask:0xf")
+OPK(k_fma_f32, "v_fma_f32 %0, %0, %1, %0")
+// mixed issue: one 32-bit + one packed 16-bit op (counted as 2 wave-instructions below)
+OPK(k_mix, "v_add_u32 %0, %0, %1\n v_pk_add_u16 %0, %0, %1")
 
 int main() {
     int dev = 0;
@@ -49,7 +61,11 @@ int main() {
         {"v_pk_add_u16", k_pk_add_u16}, {"v_pk_max_i16", k_pk_max_i16}, {"v_pk_min_u16", k_pk_min_u16},
         {"v_pk_mad_i16", k_pk_mad_i16}, {"v_perm_b32", k_perm}, {"v_xor_b32", k_xor},
         {"v_cndmask_b32", k_cndmask}, {"v_addc_co_u32", k_addc}, {"v_bfe_u32", k_bfe},
-        {"v_lshl_or_b32", k_lshl_or}, {"v_pk_add_u16(opsel)", k_pk_fma_f32_probe}};
+        {"v_lshl_or_b32", k_lshl_or}, {"v_pk_add_u16(opsel)", k_pk_fma_f32_probe},
+        {"v_pk_sub_i16 clamp", k_pk_sub_i16_clamp}, {"v_pk_maximum3_f16", k_pk_max3_f16}, {"v_bfi_b32", k_bfi},
+        {"v_pk_mad_u16", k_pk_mad_u16}, {"v_pk_max_i16(op_sel)", k_pk_max_i16_opsel},
+        {"v_mov_b32+v_add_u32 (x2)", k_mov}, {"v_mov_b32_dpp wave_shr:1", k_dpp_shr}, {"v_fma_f32", k_fma_f32},
+        {"v_add_u32+v_pk_add_u16 (x2)", k_mix}};
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
@@ -63,7 +79,8 @@ int main() {
         hipEventSynchronize(b);
         float ms;
         hipEventElapsedTime(&ms, a, b);
-        const double winstr = 5.0 * blocks * (block / 64) * (double)ITERS * CHAINS;
+        const double per = (k.f == k_mov || k.f == k_mix) ? 2.0 : 1.0;  // two instructions per chain link
+        const double winstr = per * 5.0 * blocks * (block / 64) * (double)ITERS * CHAINS;
         const double per_simd_per_s = winstr / (ms * 1e-3) / (cus * 4);
         printf("%-22s %8.3f ms  %.3f Gwave-instr/s/SIMD  => %.2f cycles/wave-instr at 2.4 GHz\n", k.n, ms,
                per_simd_per_s / 1e9, 2.4e9 / per_simd_per_s);

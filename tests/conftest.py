@@ -41,12 +41,17 @@ def digest_batch(name):
         "cfg5_semi_sample": lambda: synth.related_batch(32, 10000, 10000, 0x5EED),
         "cfg3_semi_sample": lambda: synth.cfg3_batch(64)[0],
         "cfg3_local_sample": lambda: synth.cfg3_batch(64)[0],
+        "cfg5_semi_strided": lambda: synth.related_pairs_at(synth.CFG5_STRIDED, 10000, 10000, 0x5EED),
+        "cfg3_semi_strided": lambda: synth.cfg3_batch(indices=synth.CFG3_STRIDED)[0],
+        "cfg3_local_strided": lambda: synth.cfg3_batch(indices=synth.CFG3_STRIDED)[0],
     }
     return spec[name]()
 
 
 DIGESTS = ["cfg2_local", "cfg2_related_local", "g1k_global", "s1k_semi", "ragged_local", "ragged_semi",
            "ragged_global", "cfg5_semi_sample", "cfg3_semi_sample", "cfg3_local_sample"]
+# stratified samples of the stated-size runs (pairs spread over the whole stream; the npz holds "indices")
+STRIDED = ["cfg5_semi_strided", "cfg3_semi_strided", "cfg3_local_strided"]
 
 
 def cigar_digest(res, P):

@@ -168,14 +168,15 @@ def cigar_digest(res, P):
     return h.hexdigest(), crc
 
 
-def make_digest(ref, name, batch, typ, m, n, g, desc):
+def make_digest(ref, name, batch, typ, m, n, g, desc, indices=None):
     t0 = time.time()
     res = ref.align_batch(batch, typ, m, n, g, True)
     dt = time.time() - t0
     assert not res.status.any()
     sha, crc = cigar_digest(res, batch.n_pairs)
+    extra = {} if indices is None else {"indices": np.asarray(indices, np.int64)}
     np.savez_compressed(os.path.join(OUT, f"digest_{name}.npz"), scores=res.scores, target_begins=res.target_begins,
-                        cigar_lens=res.cigar_lens, cigar_crc32=crc)
+                        cigar_lens=res.cigar_lens, cigar_crc32=crc, **extra)
     meta = {"name": name, "desc": desc, "type": typ, "match": m, "mismatch": n, "gap": g,
             "n_pairs": batch.n_pairs, "cells": batch.cells, "cigar_sha256": sha,
             "score_sum": int(res.scores.astype(np.int64).sum()), "generated_by": "oracle/_ref (reference)",
@@ -240,8 +241,26 @@ def _cfg3_local_sample(ref):
                 "synth.cfg3_batch() vs their true-origin windows, local 1/-1/-1")
 
 
+def _cfg5_strided(ref):
+    idx = synth.CFG5_STRIDED
+    make_digest(ref, "cfg5_semi_strided", synth.related_pairs_at(idx, 10000, 10000, 0x5EED), 2, 1, -1, -1,
+                "config 5 (linear gap) stratified sample: the 128 related 10kx10k pairs at stream positions "
+                "781*k (k = 0..127) of the 100,000-pair stream, semiGlobal 1/-1/-1", indices=idx)
+
+
+def _cfg3_strided(ref, mode, name):
+    idx = synth.CFG3_STRIDED
+    b, _, _ = synth.cfg3_batch(indices=idx)
+    make_digest(ref, name, b, mode, 1, -1, -1,
+                f"config 3 stand-in stratified sample: the 256 ONT-like reads at positions 39*k (k = 0..255) of the "
+                f"10,000-read set vs their true-origin windows, {MODES[mode]} 1/-1/-1", indices=idx)
+
+
 # digests added after the first set (regenerate one with --only NAME)
-DIGEST_SPECS = {"cfg3_semi_sample": _cfg3_sample, "cfg3_local_sample": _cfg3_local_sample}
+DIGEST_SPECS = {"cfg3_semi_sample": _cfg3_sample, "cfg3_local_sample": _cfg3_local_sample,
+                "cfg5_semi_strided": _cfg5_strided,
+                "cfg3_semi_strided": lambda ref: _cfg3_strided(ref, 2, "cfg3_semi_strided"),
+                "cfg3_local_strided": lambda ref: _cfg3_strided(ref, 1, "cfg3_local_strided")}
 
 
 if __name__ == "__main__":

@@ -40,7 +40,12 @@ RUNS = [
     ("grep", "rrep.fastq", ["-a", "local", "-c", "-k", "12", "-w", "3", "-m", "2", "-n", "-3", "-g", "-2"]),
     ("demo", "demo_reads.fasta", ["-c", "-k", "3", "-w", "2"]),
     ("demo", "demo_reads.fasta", ["-a", "local", "-c", "-k", "4", "-w", "3"]),
+    # pptx slide 16/17: the reference's published mapper run on its 9-bp ref.fasta
+    ("demo_ref9", "demo_reads.fasta", ["-a", "local", "-m", "2", "-n", "-1", "-g", "2", "-k", "3", "-w", "2", "-c"]),
 ]
+# the PAF lines the reference's slides publish for the last run (team_mapper.cpp:685-698)
+SLIDE17_LINES = [b"seq1\t6\t1\t6\t-\tref\t9\t0\t5\t18\t5\t60\tcg:Z:1M4D4I",
+                 b"seq2\t7\t0\t5\t+\tref\t9\t3\t8\t18\t5\t60\tcg:Z:1M4D4I"]
 
 
 def write_fasta(path, recs, width=70):
@@ -130,7 +135,8 @@ def main():
     write_fasta(os.path.join(OUT, "rrep.fasta"), rr)
     write_fastq(os.path.join(OUT, "rrep.fastq"), rr)
     # the reference's own mapper demo inputs (copied as data)
-    for src, dst in (("reference.fasta", "demo.fasta"), ("seq.fasta.txt", "demo_reads.fasta")):
+    for src, dst in (("reference.fasta", "demo.fasta"), ("seq.fasta.txt", "demo_reads.fasta"),
+                     ("ref.fasta", "demo_ref9.fasta")):
         with open(os.path.join(REF_DIR, src), "rb") as a, open(os.path.join(OUT, dst), "wb") as b:
             b.write(a.read())
     runs = []
@@ -142,6 +148,10 @@ def main():
             f.write(res.stdout)
         runs.append({"genome": gname + ".fasta", "reads": rname, "args": opts, "paf": paf,
                      "lines": res.stdout.count(b"\n")})
+        if gname == "demo_ref9":
+            for line in SLIDE17_LINES:  # the reference build reproduces its own published lines
+                assert line in res.stdout.splitlines(), (line, res.stdout)
+            runs[-1]["published_lines"] = [x.decode() for x in SLIDE17_LINES]
         print(paf, gname, rname, " ".join(opts), res.stdout.count(b"\n"), "lines")
     with open(os.path.join(OUT, "runs.json"), "w") as f:
         json.dump({"generated_by": "oracle/_ref/ref_mapper (reference Minimize + Align, restated glue)",

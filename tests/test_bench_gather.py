@@ -1,9 +1,11 @@
-"""bench.py's multi-rank result gather on CPU: world-size 2
-and 3 gloo groups run bench.ResultGather over several steps of stand-in
-plans (host tensors, ragged per-rank pair counts and CIGAR sizes); rank 0's
-gathered records and CIGAR bytes must be the rank-ordered concatenation of
-what every rank produced in the last step.  The GPU run of the same path
-(bench.py --gpus 2, 2 ranks on one device) is tests/test_bench_gpu.py."""
+"""bench.py's multi-rank result gather on CPU: world-size 2,
+3 and 4 gloo groups run bench.ResultGather over several steps of stand-in
+plans (host tensors, ragged per-rank pair counts and CIGAR sizes, one rank
+with no pairs); rank 0's gathered records and CIGAR bytes must be the
+rank-ordered concatenation of what every rank produced in the last step, and
+the other ranks must receive nothing (a gather to rank 0, not an all-gather).
+The GPU run of the same path (bench.py --gpus 2, 2 ranks on one device) is
+tests/test_bench_gpu.py."""
 import os
 import socket
 
@@ -40,7 +42,8 @@ class _FakePlan:
     def compact_cigars(self):
         allb = b"".join(self.cig)
         dst = torch.zeros(len(allb) + 37, dtype=torch.uint8)  # slack: slots are larger than the CIGARs
-        dst[:len(allb)] = torch.frombuffer(bytearray(allb), dtype=torch.uint8)
+        if allb:
+            dst[:len(allb)] = torch.frombuffer(bytearray(allb), dtype=torch.uint8)
         off = torch.zeros(self.P + 1, dtype=torch.int64)
         off[1:] = torch.cumsum(self.cigar_len.to(torch.int64), 0)
         return dst, off
@@ -61,7 +64,7 @@ def _worker(rank, world, port, q):
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
-    sizes = [7, 3, 11][:world]
+    sizes = SIZES[:world]
     g = bench.ResultGather(_FakeDist(dist, world, rank), max(sizes), True)
     for step in range(4):
         g.post(_FakePlan(rank, step, sizes[rank]))
@@ -70,11 +73,16 @@ def _worker(rank, world, port, q):
     if rank == 0:
         sc, tb, cl, cig = g.last()
         q.put((sc.tolist(), tb.tolist(), cl.tolist(), cig))
+    else:
+        q.put(("recv", rank, g.recv_bytes))
     dist.barrier()
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+SIZES = [7, 3, 11, 0]
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
 def test_result_gather_rank_order(world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -82,11 +90,14 @@ def test_result_gather_rank_order(world):
     procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
     for p in procs:
         p.start()
-    got = q.get(timeout=120)
+    msgs = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=120)
         assert p.exitcode == 0
-    sizes = [7, 3, 11][:world]
+    got = [m for m in msgs if m[0] != "recv"][0]
+    # non-root ranks received no bytes in any step
+    assert sorted((m[1], m[2]) for m in msgs if m[0] == "recv") == [(r, 0) for r in range(1, world)]
+    sizes = SIZES[:world]
     plans = [_FakePlan(r, 3, sizes[r]) for r in range(world)]
     assert got[0] == sum((p.score.tolist() for p in plans), [])
     assert got[1] == sum((p.target_begin.tolist() for p in plans), [])

@@ -109,9 +109,11 @@ def _runs():
         return json.load(f)["runs"]
 
 
-@pytest.mark.parametrize("run", range(9))
+@pytest.mark.parametrize("run", range(10))
 def test_mapper_cli_matches_reference_paf(run):
     r = _runs()[run]
+    for line in r.get("published_lines", []):  # run9: the reference's own slide-17 lines, literally
+        assert line.encode() in open(os.path.join(MG, r["paf"]), "rb").read().splitlines()
     res = M.run_cli(r["args"] + [os.path.join(MG, r["genome"]), os.path.join(MG, r["reads"])], timeout=120)
     assert res.returncode == 0, res.stderr.decode()
     want = open(os.path.join(MG, r["paf"]), "rb").read()
@@ -120,6 +122,17 @@ def test_mapper_cli_matches_reference_paf(run):
         gl, wl = got.splitlines(), want.splitlines()
         diff = [(a[:160], b[:160]) for a, b in zip(gl, wl) if a != b][:3]
         raise AssertionError(f"{r['paf']}: {len(gl)} vs {len(wl)} lines; first diffs {diff}")
+
+
+def test_mapper_slide17_published_lines():
+    """pptx slide 16/17: `-a local -m 2 -n -1 -g 2 -k 3 -w 2 -c ref.fasta seq.fasta.txt`
+    prints these two lines (team_mapper.cpp:685-698); team_mapper_amd prints them too."""
+    r = [x for x in _runs() if x["genome"] == "demo_ref9.fasta"][0]
+    res = M.run_cli(r["args"] + [os.path.join(MG, r["genome"]), os.path.join(MG, r["reads"])], timeout=120)
+    assert res.returncode == 0, res.stderr.decode()
+    got = res.stdout.splitlines()
+    assert b"seq1\t6\t1\t6\t-\tref\t9\t0\t5\t18\t5\t60\tcg:Z:1M4D4I" in got
+    assert b"seq2\t7\t0\t5\t+\tref\t9\t3\t8\t18\t5\t60\tcg:Z:1M4D4I" in got
 
 
 def test_map_batch_api_matches_cli(mp):

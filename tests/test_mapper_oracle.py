@@ -40,6 +40,25 @@ def test_mapper_fixtures_present():
         assert open(os.path.join(MG, r["paf"]), "rb").read().count(b"\n") == r["lines"]
 
 
+def test_slide17_published_paf_fixture():
+    """run9 is the reference's published mapper run (pptx slide 16/17,
+    `-a local -m 2 -n -1 -g 2 -k 3 -w 2 -c ref.fasta seq.fasta.txt`): its PAF
+    fixture holds the two published lines literally."""
+    with open(os.path.join(MG, "runs.json")) as f:
+        r = [x for x in json.load(f)["runs"] if x["genome"] == "demo_ref9.fasta"][0]
+    assert r["args"] == ["-a", "local", "-m", "2", "-n", "-1", "-g", "2", "-k", "3", "-w", "2", "-c"]
+    lines = open(os.path.join(MG, r["paf"]), "rb").read().splitlines()
+    assert b"seq1\t6\t1\t6\t-\tref\t9\t0\t5\t18\t5\t60\tcg:Z:1M4D4I" in lines
+    assert b"seq2\t7\t0\t5\t+\tref\t9\t3\t8\t18\t5\t60\tcg:Z:1M4D4I" in lines
+    if pm.RefMapper.available():  # the reference build (oracle/_ref/ref_mapper) reproduces the fixture
+        import subprocess
+
+        res = subprocess.run([pm.REF_MAPPER_BIN] + r["args"] + [os.path.join(MG, r["genome"]),
+                                                                os.path.join(MG, r["reads"])],
+                             capture_output=True, check=True, timeout=60)
+        assert res.stdout.splitlines() == lines
+
+
 @pytest.mark.skipif(not pm.RefMapper.available(), reason="oracle/_ref not built (reference sources absent)")
 def test_restatement_vs_reference_fuzz():
     ref = pm.RefMapper()

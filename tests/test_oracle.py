@@ -5,7 +5,7 @@ reproduce all of them bit for bit -- scores, CIGAR bytes (incl. the "1\\0"
 empty case), target_begin and the two error messages."""
 import numpy as np
 import pytest
-from conftest import DIGESTS, cigar_digest, digest_batch, load_digest
+from conftest import DIGESTS, STRIDED, cigar_digest, digest_batch, load_digest
 
 from oracle.pyoracle import AlignError, Oracle, Reference
 
@@ -60,6 +60,31 @@ def test_digest(oracle, name):
     sha, crc = cigar_digest(res, batch.n_pairs)
     np.testing.assert_array_equal(crc, d["cigar_crc32"])
     assert sha == meta["cigar_sha256"]
+
+
+@pytest.mark.parametrize("name", STRIDED)
+def test_strided_digest(oracle, name):
+    """The stratified digests (pairs spread over the stated-size streams): the
+    regenerated inputs match the digest's cell count, and every 4th sampled
+    pair (32 of config 5's 10 kb x 10 kb pairs, 64 config-3 reads per mode; the
+    whole sample runs on the GPU, tests/test_gpu_parity.py) is bit-exact."""
+    import zlib
+
+    from bioinfo1_amd import synth
+
+    meta, d = load_digest(name)
+    batch = digest_batch(name)
+    assert batch.n_pairs == meta["n_pairs"] == len(d["indices"]) and batch.cells == meta["cells"]
+    want_idx = synth.CFG5_STRIDED if name.startswith("cfg5") else synth.CFG3_STRIDED
+    np.testing.assert_array_equal(d["indices"], want_idx)
+    pick = np.arange(0, batch.n_pairs, 4)
+    sub = synth.from_pairs([(batch.query(int(p)), batch.target(int(p))) for p in pick])
+    res = oracle.align_batch(sub, meta["type"], meta["match"], meta["mismatch"], meta["gap"], True)
+    assert not res.status.any()
+    np.testing.assert_array_equal(res.scores, d["scores"][pick])
+    np.testing.assert_array_equal(res.target_begins, d["target_begins"][pick])
+    np.testing.assert_array_equal(res.cigar_lens, d["cigar_lens"][pick])
+    assert [zlib.crc32(res.cigar(k)) for k in range(len(pick))] == [int(x) for x in d["cigar_crc32"][pick]]
 
 
 @pytest.mark.skipif(not Reference.available(), reason="oracle/_ref not built (reference sources absent)")
