@@ -300,8 +300,12 @@ class ResultGather:
                     w = dst[:4 * words].view(torch.int32) if self.nccl else dst[:4 * words].cpu().view(torch.int32)
                     st["send"] = w
                     ops.append(D.dist.P2POp(D.dist.isend, w, 0))
-            if ops:
+            if ops and self.nccl:
                 st["works"] += D.dist.batch_isend_irecv(ops)
+            for op in ops if not self.nccl else ():
+                # gloo (the CPU / one-GPU rehearsal): blocking transfers -- a large asynchronous
+                # send left in flight under the next step's gather stalls gloo's pair
+                (D.dist.recv if op.op is D.dist.irecv else D.dist.send)(op.tensor, op.peer)
         st["bytes"] = True
 
     def drain(self):

@@ -16,13 +16,18 @@ pids=()
 # incremental: an object is rebuilt when its source or any csrc header is newer (TA_FORCE=1: always)
 if [ "$(cat "$B/.flags" 2>/dev/null)" != "${FLAGS[*]}" ]; then TA_FORCE=1; fi  # other flags: rebuild all
 echo "${FLAGS[*]}" > "$B/.flags"
-HNEW=$(ls -t "$CS"/*.h "$ROOT"/include/*.h* 2>/dev/null | sed -n 1p)
-stale() {  # stale <obj> <src>
-  [ "${TA_FORCE:-0}" = 1 ] || [ ! -f "$1" ] || [ "$2" -nt "$1" ] || [ "$HNEW" -nt "$1" ] || [ "$0" -nt "$1" ]
+stale() {  # stale <obj> <src>: missing, or older than its source / a header it includes (<obj>.d)
+  [ "${TA_FORCE:-0}" = 1 ] || [ ! -f "$1" ] || [ ! -f "$1.d" ] || [ "$2" -nt "$1" ] || [ "$0" -nt "$1" ] && return 0
+  local dep
+  for dep in $(sed -e 's/^[^:]*://' -e 's/\\$//' "$1.d"); do
+    case "$dep" in /opt/*|/usr/*) continue ;; esac
+    [ "$dep" -nt "$1" ] && return 0
+  done
+  return 1
 }
-cc() {  # cc <obj> <src> <compiler args...>: background compile when stale
+cc() {  # cc <obj> <src> <compiler args...>: background compile when stale (dependencies into <obj>.d)
   local o="$1" src="$2"; shift 2
-  if stale "$o" "$src"; then "$@" -o "$o" & pids+=($!); fi
+  if stale "$o" "$src"; then "$@" -MD -MF "$o.d" -o "$o" & pids+=($!); fi
 }
 for m in 0 1 2; do
   for c in 0 1; do

@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""The VALU issue roof of a fill kernel, from measured per-opcode rates.
+
+  python scripts/valu_roof.py [--rates profiles/r03_valu_rates.txt] [--out profiles/valu_roof.json]
+
+1. Per-opcode issue cost: scripts/exp/ubench/valu_rates (run on the MI355X)
+   prints cycles per wave64 instruction per SIMD for the opcodes the kernels
+   use (8 independent chains x 8 waves per SIMD: throughput, not latency).
+   The measured values sit ~5-30 % above the issue class (loop overhead);
+   each opcode is assigned its class, 2 or 4 cycles (the nearest of 2, 4, 8, 16).
+2. Instruction mix: a static census of the kernel's hot loop (the loop with the
+   most DPP hand-offs) in the gfx950 assembly of its translation unit.
+3. Mixed roof: cycles per wave-instruction = census-weighted mean of the
+   classes; peak = 256 CU x 4 SIMD x 64 lanes x 2.4 GHz / that mean, in VALU
+   lane-operations per second -- the number bench.py's valu.frac divides by.
+Opcodes the ubench does not cover count as 2 cycles (packed ones as 4): that
+can only raise the roof, i.e. lower the reported fraction."""
+from __future__ import annotations
+
+import argparse
+import collections
+import json
+import os
+import re
+import subprocess
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+CS = os.path.join(ROOT, "bioinfo1_amd", "csrc")
+SIMDS, CLOCK = 256 * 4, 2.4e9
+
+# kernel tag -> (source, defines, kernel symbol substring)
+KERNELS = {
+    "dual_fill_kernel<kLocal,true>": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1"], "dual_fill_kernelILi1ELb1E"),
+    "dual_fill_kernel<kSemi,true>": ("ta_dual.hip", ["-DTA_DUAL_MODE=2", "-DTA_DUAL_CIGAR=1"], "dual_fill_kernelILi2ELb1E"),
+    "flex_fill_kernel<kSemi,true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=2", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi2ELb1E"),
+    "flex_fill_kernel<kLocal,true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=1", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi1ELb1E"),
+    "affine_dual_fill_kernel<kSemi,true>": ("ta_affine.hip", [], "affine_dual_fill_kernelILi2ELb1E"),
+}
+
+
+def parse_rates(path):
+    rates = {}
+    for ln in open(path):
+        m = re.match(r"^(\S.*?)\s+[\d.]+ ms .*=> ([\d.]+) cycles", ln)
+        if not m:
+            continue
+        name, cyc = m.group(1).strip(), float(m.group(2))
+        if "(x2)" in name:  # two instructions per link: name the first opcode only when the second is known
+            continue
+        name = name.split(" ")[0].split("(")[0]
+        rates.setdefault(name, cyc)
+    return rates
+
+
+def issue_class(c):
+    return min((2, 4, 8, 16), key=lambda k: abs(k - c))
+
+
+def base_op(op):
+    op = re.sub(r"_(e32|e64|sdwa|dpp)$", "", op)
+    return op
+
+
+def census(src, defines, sym):
+    out = "/tmp/valu_roof"
+    os.makedirs(out, exist_ok=True)
+    stem = src.rsplit(".", 1)[0]
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", *defines, "-c",
+                           os.path.join(CS, src), "-o", f"{out}/k.o", "-save-temps"], cwd=out,
+                          stderr=subprocess.DEVNULL)
+    text = open(f"{out}/{stem}-hip-amdgcn-amd-amdhsa-gfx950.s").read()
+    funcs = re.split(r"\n(?=_Z\w+:)", text)
+    body = [f for f in funcs if f.split(":")[0].find(sym) >= 0 and "s_endpgm" in f][0].split(".Lfunc_end")[0]
+    lines = body.splitlines()
+    labels = {m.group(1): k for k, ln in enumerate(lines) if (m := re.match(r"^(\.LBB\w+):", ln))}
+    best = None
+    for k, ln in enumerate(lines):
+        m = re.search(r"s_cbranch_\w+\s+(\.LBB\w+)|s_branch\s+(\.LBB\w+)", ln)
+        if m:
+            t = m.group(1) or m.group(2)
+            if t in labels and labels[t] < k:
+                c = collections.Counter()
+                for x in lines[labels[t]:k + 1]:
+                    tok = x.strip().split()
+                    if tok and tok[0].startswith("v_"):
+                        c[tok[0]] += 1
+                dpp = sum(v for o, v in c.items() if "_dpp" in o)
+                if best is None or dpp > best[0]:
+                    best = (dpp, c)
+    return best[1]
+
+
+def roof(mix, rates):
+    tot = cyc = 0.0
+    per = {}
+    for op, n in mix.items():
+        b = base_op(op)
+        if op.endswith("_dpp"):
+            b = "v_mov_b32_dpp" if op.startswith("v_mov") else b
+        meas = rates.get(b)
+        if meas is None and op.endswith("_dpp"):
+            meas = rates.get("v_mov_b32_dpp")
+        k = issue_class(meas) if meas is not None else (4 if b.startswith("v_pk_") else 2)
+        per[op] = {"count": n, "measured_cycles": meas, "class_cycles": k}
+        tot += n
+        cyc += n * k
+    mean = cyc / tot
+    return mean, per
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rates", default=os.path.join(ROOT, "profiles", "r03_valu_rates.txt"))
+    ap.add_argument("--out", default=os.path.join(ROOT, "profiles", "valu_roof.json"))
+    a = ap.parse_args()
+    rates = parse_rates(a.rates)
+    res = {"rates_source": os.path.relpath(a.rates, ROOT), "method": __doc__.split("\n\n")[1].strip(),
+           "kernels": {}}
+    for tag, (src, defs, sym) in KERNELS.items():
+        mix = census(src, defs, sym)
+        mean, per = roof(mix, rates)
+        peak = SIMDS * 64 * CLOCK / mean / 1e12
+        four = sum(v["count"] for v in per.values() if v["class_cycles"] >= 4) / sum(v["count"] for v in per.values())
+        res["kernels"][tag] = {"mean_cycles_per_wave_instr": round(mean, 3), "peak_lane_tops": round(peak, 2),
+                               "share_4cycle_ops": round(four, 3), "hot_loop_valu_instrs": sum(mix.values()),
+                               "mix": dict(sorted(per.items(), key=lambda kv: -kv[1]["count"]))}
+        print(f"{tag}: mean {mean:.3f} cycles/wave-instr, 4-cycle share {four:.2f}, peak {peak:.1f} T lane-ops/s")
+    with open(a.out, "w") as f:
+        json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -30,12 +30,12 @@ class _FakeDist:
 class _FakePlan:
     """What ResultGather reads from a DevicePlan, for one rank and one step."""
 
-    def __init__(self, rank, step, n):
+    def __init__(self, rank, step, n, max_len=40):
         rng = np.random.default_rng(1000 * rank + step)
         self.P = n
         self.score = torch.from_numpy(rng.integers(-50, 50, n).astype(np.int32))
         self.target_begin = torch.from_numpy(rng.integers(0, 9, n).astype(np.int32))
-        lens = rng.integers(1, 40, n).astype(np.int32)
+        lens = rng.integers(1, max_len, n).astype(np.int32)
         self.cigar_len = torch.from_numpy(lens)
         self.cig = [bytes(rng.integers(48, 90, int(k)).astype(np.uint8)) for k in lens]
 
@@ -57,7 +57,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, q):
+def _worker(rank, world, port, q, max_len=40):
     import torch.distributed as dist
 
     import bench
@@ -66,8 +66,12 @@ def _worker(rank, world, port, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     sizes = SIZES[:world]
     g = bench.ResultGather(_FakeDist(dist, world, rank), max(sizes), True)
-    for step in range(4):
-        g.post(_FakePlan(rank, step, sizes[rank]))
+    # bench.py's sequence: warmup step, drain, barrier, timed steps, drain
+    g.post(_FakePlan(rank, 0, sizes[rank], max_len))
+    g.drain()
+    dist.barrier()
+    for step in range(1, 4):
+        g.post(_FakePlan(rank, step, sizes[rank], max_len))
         g.clear_old()
     g.drain()
     if rank == 0:
@@ -82,12 +86,14 @@ def _worker(rank, world, port, q):
 SIZES = [7, 3, 11, 0]
 
 
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_result_gather_rank_order(world):
+@pytest.mark.parametrize("world,max_len", [(2, 40), (3, 40), (4, 40), (2, 400000)])
+def test_result_gather_rank_order(world, max_len):
+    """max_len 400000: MB-sized CIGAR byte transfers per rank and step (a config-4
+    slice), which once stalled gloo when left in flight under the next gather."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q, max_len)) for r in range(world)]
     for p in procs:
         p.start()
     msgs = [q.get(timeout=120) for _ in range(world)]
@@ -98,7 +104,7 @@ def test_result_gather_rank_order(world):
     # non-root ranks received no bytes in any step
     assert sorted((m[1], m[2]) for m in msgs if m[0] == "recv") == [(r, 0) for r in range(1, world)]
     sizes = SIZES[:world]
-    plans = [_FakePlan(r, 3, sizes[r]) for r in range(world)]
+    plans = [_FakePlan(r, 3, sizes[r], max_len) for r in range(world)]
     assert got[0] == sum((p.score.tolist() for p in plans), [])
     assert got[1] == sum((p.target_begin.tolist() for p in plans), [])
     assert got[2] == sum((p.cigar_len.tolist() for p in plans), [])
