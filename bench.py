@@ -55,9 +55,11 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, Chip-level parameters)
-# int32 VALU: a wave64 integer instruction occupies its SIMD for 4 cycles (measured:
-# SQ_ACTIVE_INST_VALU == SQ_INSTS_VALU quad-cycles at ~100% busy), i.e. 16 lanes/clk/SIMD:
-# 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T lane-ops/s
+# VALU issue roof of the dominant fill kernel: profiles/valu_roof.json (scripts/valu_roof.py) weights the
+# measured issue cost of every opcode of the kernel's hot loop (scripts/exp/ubench/valu_rates on the
+# MI355X: packed 16-bit ops, v_perm/v_bfi/v_max*/DPP 4 cycles per wave64 instruction, v_add/v_xor/
+# v_mov/v_cmp 2) by the kernel's instruction mix.  Fallback when a kernel has no entry: every
+# instruction 4 cycles, 256 CU x 4 SIMD x 16 lanes x 2.4 GHz = 39.3 T lane-ops/s.
 VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 METRIC = "GCUPS (DP cell updates/s) at 1/2/4/8 GPUs; bit-exact score+CIGAR"
 MODES = {"global": 0, "local": 1, "semiGlobal": 2}
@@ -685,9 +687,16 @@ def main_align(args, D):
                                    "ops/cell are rocprof per-dispatch averages x launches_per_step",
                 "note": "integer DP: VALU-bound, not HBM- or MFMA-bound (see valu)"}
         ops = load_profile("valu.json", tag)
+        kroof = (load_profile("valu_roof.json", "kernels") or {}).get(roof["kernel"])
+        peak = kroof["peak_lane_tops"] if kroof else VALU_PEAK_TOPS
         valu = {"kernel_gcups": round(batch.cells / (fill_ms / 1e3) / 1e9, 2),
-                "peak_int32_tops": round(VALU_PEAK_TOPS, 1), "valu_ops_per_cell": ops,
-                "frac": round(batch.cells * ops / (fill_ms / 1e3) / 1e12 / VALU_PEAK_TOPS, 4) if ops else None}
+                "peak_lane_tops": round(peak, 2),
+                "peak_basis": ("profiles/valu_roof.json: measured per-opcode issue cost (profiles/r03_valu_rates.txt) "
+                               f"weighted by the kernel's instruction mix, {kroof['mean_cycles_per_wave_instr']} "
+                               "cycles per wave64 instruction") if kroof else "every instruction 4 cycles (fallback)",
+                "valu_ops_per_cell": ops,
+                "achieved_lane_tops": round(batch.cells * ops / (fill_ms / 1e3) / 1e12, 2) if ops else None,
+                "frac": round(batch.cells * ops / (fill_ms / 1e3) / 1e12 / peak, 4) if ops else None}
         extra = {}
         if gathered is not None:
             extra["gather"] = check_gathered(args, gathered, plan, full, al, mode, sc, cigar)

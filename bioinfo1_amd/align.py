@@ -26,7 +26,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libteam_alignment.so")
 
-TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY, TA_ERR_RANGE = range(7)
+TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY, TA_ERR_RANGE, TA_ERR_UNSERVED = range(8)
 # ta_plan_create flags (include/team_align_c.h): kernel selection, same results
 TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2 = 1, 2, 4, 8, 16
 
@@ -78,6 +78,7 @@ def lib() -> C.CDLL:
     L.ta_context_release.restype = None
     L.ta_context_held_bytes.argtypes = [C.c_void_p]
     L.ta_context_held_bytes.restype = C.c_uint64
+    L.ta_set_default_device.argtypes = [C.c_int]
     L.ta_plan_create.argtypes = [C.c_void_p, C.c_uint32, u32p, u32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p)]
     L.ta_plan_destroy.argtypes = [C.c_void_p]
@@ -118,6 +119,15 @@ def lib() -> C.CDLL:
     L.ta_affine_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ta_affine_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     L.ta_affine_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+    # the low-latency single-pair server (ta_server_*)
+    L.ta_server_create.argtypes = [C.c_int, C.c_int, C.c_uint32, C.POINTER(C.c_void_p)]
+    L.ta_server_destroy.argtypes = [C.c_void_p]
+    L.ta_server_destroy.restype = None
+    L.ta_server_fits.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int]
+    L.ta_server_running.argtypes = [C.c_void_p]
+    L.ta_server_align.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_int, C.c_int,
+                                  C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.c_void_p,
+                                  C.c_uint64, C.POINTER(C.c_uint32)]
     _lib = L
     return L
 
@@ -125,13 +135,14 @@ def lib() -> C.CDLL:
 # Every symbol include/team_align_c.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = [
     "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_context_release",
-    "ta_context_held_bytes",
+    "ta_context_held_bytes", "ta_set_default_device", "ta_current_device", "ta_device_count",
     "ta_cigar_slot_bytes", "ta_align_batch", "ta_align_batch_flags", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes",
     "ta_plan_workspace_bytes", "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_fused",
     "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_pair_chunks", "ta_affine_plan_pair_chunks", "ta_plan_execute_traceback", "ta_compact_cigars",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
     "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
+    "ta_server_create", "ta_server_destroy", "ta_server_fits", "ta_server_align", "ta_server_running",
 ]
 # The drop-in C++ entry point (team_alignment.hpp), g++/libstdc++ cxx11 mangling.
 TEAM_ALIGN_SYMBOL = ("_ZN4team5AlignEPKcjS1_jNS_13AlignmentTypeEiiiPNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEEPj")
@@ -272,6 +283,53 @@ def align_affine(query: bytes, target: bytes, type, match: int, mismatch: int, g
     res = default_aligner().align_batch_affine(from_pairs([(bytes(query), bytes(target))]), type, match, mismatch,
                                                gap_open, gap_extend, want_cigar)
     return int(res.scores[0]), res.cigar(0), int(res.target_begins[0])
+
+
+class Server:
+    """The low-latency single-pair path (ta_server_*): a resident kernel, one
+    wave per slot, serves one team::Align call at a time per slot -- what the
+    drop-in team::Align uses for pairs up to 4096 x 16384.  align() returns
+    (score, cigar bytes or None, target_begin) like align(); a pair outside
+    the server's limits raises LookupError (the caller takes a batch)."""
+
+    def __init__(self, device: int, type, slots: int = 32):
+        L = lib()
+        h = C.c_void_p()
+        r = L.ta_server_create(device, _check_type(type), slots, C.byref(h))
+        if r != TA_OK:
+            _raise(r)
+        self._h = h
+        self.type = int(type)
+
+    def fits(self, n: int, m: int, match: int, mismatch: int, gap: int) -> bool:
+        return bool(lib().ta_server_fits(self._h, n, m, match, mismatch, gap))
+
+    def running(self) -> bool:
+        return bool(lib().ta_server_running(self._h))
+
+    def align(self, query: bytes, target: bytes, match: int, mismatch: int, gap: int, want_cigar: bool = True):
+        query, target = bytes(query), bytes(target)
+        cap = 2 * (len(query) + len(target)) + 2
+        buf = C.create_string_buffer(cap) if want_cigar else None
+        sc, tb, cl = C.c_int32(0), C.c_uint32(0), C.c_uint32(0)
+        r = lib().ta_server_align(self._h, query, len(query), target, len(target), match, mismatch, gap,
+                                  int(bool(want_cigar)), C.byref(sc), C.byref(tb), buf, cap, C.byref(cl))
+        if r == TA_ERR_UNSERVED:
+            raise LookupError("pair outside the single-pair server's limits")
+        if r != TA_OK:
+            _raise(r)
+        return sc.value, (buf.raw[: cl.value] if want_cigar else None), tb.value
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().ta_server_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 class _DeviceIO(C.Structure):

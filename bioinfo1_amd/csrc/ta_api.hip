@@ -320,6 +320,7 @@ const char* ta_status_string(int status) {
         case TA_ERR_DEVICE: return "device error";
         case TA_ERR_CAPACITY: return "cigar arena too small";
         case TA_ERR_RANGE: return "affine scoring out of range";
+        case TA_ERR_UNSERVED: return "pair outside the single-pair server's limits";
         default: return "unknown status";
     }
 }
@@ -362,10 +363,22 @@ void ta_context_release(ta_context* ctx) {
     for (auto* b : {&ctx->pin_in, &ctx->pin_out}) ta_host::release(*b, true);
 }
 
+int ta_current_device(void) {
+    int d = 0;
+    return hipGetDevice(&d) == hipSuccess ? d : 0;
+}
+
+int ta_device_count(void) {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess ? n : 0;
+}
+
 uint64_t ta_context_held_bytes(const ta_context* ctx) {
     if (!ctx) return 0;
     uint64_t n = 0;
-    for (const auto* b : {&ctx->blk, &ctx->out, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd}) n += b->cap;
+    // only what a plan's workspace can reuse: the code and pass-boundary buffers
+    // (staging and output buffers are not handed to a plan's chunks)
+    for (const auto* b : {&ctx->ws_ptrs, &ctx->ws_bnd}) n += b->cap;
     return n;
 }
 

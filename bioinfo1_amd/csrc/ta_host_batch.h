@@ -71,6 +71,24 @@ inline int check_host_batch(ta_context* ctx, int type, uint32_t n_pairs, const c
     return TA_OK;
 }
 
+// After the first enqueue an early return (a failed HIP call or plan execute)
+// must not leave work in flight on the context's stream: the next call packs
+// its inputs into the same pinned staging that an unfinished upload may still
+// read.  The guard drains the stream and records the context's last event.
+struct StreamGuard {
+    ta_context* ctx;
+    hipStream_t s;
+    bool armed = true;
+    ~StreamGuard() {
+        if (!armed) return;
+        (void)hipStreamSynchronize(s);
+        if (hipEventRecord(ctx->ev_last, s) == hipSuccess) {
+            ctx->last_stream = s;
+            ctx->used = true;
+        }
+    }
+};
+
 // Called with ctx->mu held.
 inline int host_batch(ta_context* ctx, HostPlan& hp, uint32_t n_pairs, const char* qb, const uint64_t* qoff,
                       const uint32_t* qlen, const char* tbytes, const uint64_t* toff, const uint32_t* tlen,
@@ -100,6 +118,7 @@ inline int host_batch(ta_context* ctx, HostPlan& hp, uint32_t n_pairs, const cha
         if (tend) std::memcpy(hin + o_tb, tbytes, tend);
     }
     if (int r = stream_enter(ctx, s)) return r;
+    StreamGuard guard{ctx, s};
     roctxRangePushA("ta upload");
     TA_HIP(ctx, hipMemcpyAsync(d, hin, upload, hipMemcpyHostToDevice, s));
     if (!pack_seq) {  // pinned or pageable caller memory: HIP picks the path
@@ -137,6 +156,7 @@ inline int host_batch(ta_context* ctx, HostPlan& hp, uint32_t n_pairs, const cha
     TA_HIP(ctx, hipStreamSynchronize(s));
     roctxRangePop();
     if (int r = stream_leave(ctx, s)) return r;
+    guard.armed = false;  // drained and recorded (the compaction below synchronises itself)
     if (err_off != UINT64_MAX) {
         uint32_t err = 0;
         std::memcpy(&err, hout + down, 4);
@@ -161,12 +181,14 @@ inline int host_batch(ta_context* ctx, HostPlan& hp, uint32_t n_pairs, const cha
             if (int r = grow(ctx, ctx->dst, total + P * 8 + 256)) return r;
             uint8_t* dd = static_cast<uint8_t*>(ctx->dst.p);
             const uint64_t o_dst = (P * 8 + 255) & ~uint64_t(255);
+            guard.armed = true;
             TA_HIP(ctx, hipMemcpyAsync(dd, ctx->pin_in.p, P * 8, hipMemcpyHostToDevice, s));
             ta::CompactArgs ca{n_pairs, io.cigar_slots, io.cigar_start, io.cigar_len,
                                reinterpret_cast<const uint64_t*>(dd), reinterpret_cast<char*>(dd + o_dst)};
             TA_HIP(ctx, ta::launch_compact(ca, s));
             TA_HIP(ctx, hipMemcpyAsync(arena, dd + o_dst, total, hipMemcpyDeviceToHost, s));
             TA_HIP(ctx, hipStreamSynchronize(s));
+            guard.armed = false;
         }
     }
     if (score) std::memcpy(score, hout + o_sc, P * 4);

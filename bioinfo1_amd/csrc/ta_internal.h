@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "../../include/team_align_c.h"
 #include "ta_layout.h"
 
 namespace ta {
@@ -90,6 +91,45 @@ struct CompactArgs {
     char* dst;
 };
 
+// ---- the low-latency single-pair server (ta_server.cpp, serve_kernel in ta_kernels.hip)
+// A persistent kernel, one wave per slot, serves team::Align calls posted in
+// fine-grained pinned host memory: the host writes a request (lengths,
+// scoring, sequence bytes) and bumps `seq`; the wave copies the bytes to HBM,
+// fills and walks the pair (the int32 fill with its walk fused), writes the
+// results and CIGAR back into the slot and sets `done = seq`.  No launch and
+// no copy per call.
+constexpr uint32_t kSrvQMax = 4096;       // query rows a slot takes (4 passes)
+constexpr uint32_t kSrvTMax = 16384;      // target columns
+constexpr uint64_t kSrvStride = 65536;    // bytes per host slot: header, query, target, CIGAR
+constexpr uint64_t kSrvQOff = 128, kSrvTOff = kSrvQOff + kSrvQMax, kSrvCOff = kSrvTOff + kSrvTMax;
+static_assert(kSrvCOff + 2 * (kSrvQMax + kSrvTMax) + 2 <= kSrvStride, "server slot too small");
+
+struct ServeHdr {           // the first 128 bytes of a host slot
+    uint32_t seq;            // host: number of the posted request (written last)
+    uint32_t n, m;           // host: lengths
+    int32_t match, mismatch, gap;
+    uint32_t want_cigar;
+    uint32_t pad0[9];
+    uint32_t done;           // device: seq of the last finished request (written last)
+    int32_t score;
+    uint32_t target_begin, cigar_len, status;
+    uint32_t pad1[11];
+};
+static_assert(sizeof(ServeHdr) == kSrvQOff, "ServeHdr layout");
+
+struct ServeCtl {            // pinned host control words shared by the slots
+    uint32_t stop;           // host: the waves exit
+    uint32_t heartbeat;      // host: incremented every ~1 ms while the server is wanted
+    uint32_t pad[14];
+};
+
+struct ServeArgs {
+    char* host;              // slot s at host + s * kSrvStride (fine-grained pinned memory)
+    const ServeCtl* ctl;
+    FillArgs fa;             // per-slot device arrays, pair index = slot (qlen/tlen written per request)
+    uint64_t hb_timeout;     // wall-clock ticks (100 MHz) without a heartbeat before a wave exits
+};
+
 // Launchers (ta_kernels.hip).  `wide` selects the unscaled local-mode kernel
 // (needed only when |scores| could reach 2^25; see run_pass SCALED).
 hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s);
@@ -108,5 +148,9 @@ hipError_t launch_flex(int mode, bool cigar, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_flex_mode(const FillArgs& a, hipStream_t s);
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s);
+// The server of one mode (slots waves, one per block): returns once launched.
+template <int MODE>
+hipError_t launch_serve_mode(const ServeArgs& a, uint32_t slots, hipStream_t s);
+hipError_t launch_serve(int mode, const ServeArgs& a, uint32_t slots, hipStream_t s);
 
 }  // namespace ta

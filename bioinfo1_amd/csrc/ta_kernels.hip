@@ -328,12 +328,9 @@ __device__ __forceinline__ PassOut run_pass_any(const FillArgs& a, const uint8_t
     return run_pass_nv<MODE, CIGAR, WIDE, false>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
 }
 
+// The fill of pair p by one wave (all passes), its goal cell and, fused, its walk.
 template <int MODE, bool CIGAR, bool WIDE>
-__global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
-    const int lane = threadIdx.x & 63;
-    const uint32_t widx = wave_id();
-    if (widx >= (a.count_dev ? *a.count_dev : a.count)) return;  // wave-uniform
-    const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
+__device__ __forceinline__ void fill_pair(const FillArgs& a, uint32_t p, int lane) {
     const uint32_t n = a.qlen[p], m = a.tlen[p];
     if (n == 0 || m == 0) {
         if (lane == 0) degenerate<MODE>(a, p, n, m);
@@ -385,6 +382,110 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
         a.goal_j[p] = (MODE == kGlobal) ? m : best_j;
     }
 }
+
+template <int MODE, bool CIGAR, bool WIDE>
+__global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
+    const int lane = threadIdx.x & 63;
+    const uint32_t widx = wave_id();
+    if (widx >= (a.count_dev ? *a.count_dev : a.count)) return;  // wave-uniform
+    fill_pair<MODE, CIGAR, WIDE>(a, a.order ? a.order[a.begin + widx] : a.begin + widx, lane);
+}
+
+#if TA_FILL_CIGAR
+// ---- the low-latency server (ta_internal.h ServeArgs; host side ta_server.cpp)
+__device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One request of slot s: copy the bytes into HBM, fill + walk, results back.
+template <int MODE>
+__device__ __forceinline__ void serve_one(const ServeArgs& sa, uint32_t s, char* slot, uint32_t seq, int lane) {
+    ServeHdr* hd = reinterpret_cast<ServeHdr*>(slot);
+    const uint32_t* req = reinterpret_cast<const uint32_t*>(slot);
+    // words 1..6: n, m, match, mismatch, gap, want_cigar (one round trip)
+    const uint32_t w = (lane < 6) ? sys_load(req + 1 + lane) : 0u;
+    const uint32_t n = (uint32_t)rdlane((int)w, 0), m = (uint32_t)rdlane((int)w, 1);
+    const int ma = rdlane((int)w, 2), mi = rdlane((int)w, 3), gap = rdlane((int)w, 4);
+    const bool want = rdlane((int)w, 5) != 0;
+    FillArgs a = sa.fa;
+    uint32_t status = TA_OK;
+    int score = 0;
+    uint32_t tb = 0, clen = 0;
+    if (n > kSrvQMax || m > kSrvTMax) {
+        status = TA_ERR_ARG;  // (the host never posts such a pair)
+    } else {
+        uint8_t* dq = const_cast<uint8_t*>(a.qbytes) + a.qoff[s];
+        uint8_t* dt = const_cast<uint8_t*>(a.tbytes) + a.toff[s];
+        for (uint32_t k = 16u * (uint32_t)lane; k < n; k += 1024u)
+            *reinterpret_cast<uint4*>(dq + k) = *reinterpret_cast<const uint4*>(slot + kSrvQOff + k);
+        for (uint32_t k = 16u * (uint32_t)lane; k < m; k += 1024u)
+            *reinterpret_cast<uint4*>(dt + k) = *reinterpret_cast<const uint4*>(slot + kSrvTOff + k);
+        if (lane == 0) {
+            const_cast<uint32_t*>(a.qlen)[s] = n;
+            const_cast<uint32_t*>(a.tlen)[s] = m;
+        }
+        __threadfence();  // this wave's stores -> its own loads in the fill
+        a.match = ma;
+        a.mismatch = mi;
+        a.gap = gap;
+        a.fused = want ? 1 : 0;
+        fill_pair<MODE, true, false>(a, s, lane);
+        __threadfence();
+        score = a.score[s];
+        tb = a.target_begin[s];
+        if (want) {
+            clen = a.cigar_len[s];
+            const char* src = a.slots + a.cigar_start[s];
+            for (uint32_t k = (uint32_t)lane; k < clen; k += 64u) slot[kSrvCOff + k] = src[k];
+        }
+    }
+    if (lane == 0) {
+        hd->score = score;
+        hd->target_begin = tb;
+        hd->cigar_len = clen;
+        hd->status = status;
+    }
+    __threadfence_system();  // results and CIGAR bytes visible to the host before `done`
+    if (lane == 0) __hip_atomic_store(&hd->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// One wave per slot (block).  Polls its slot's `seq`, the stop flag and the
+// heartbeat in one round trip; exits on stop, or when the heartbeat has not
+// moved for hb_timeout (the host process is gone or hung): every wave ends.
+template <int MODE>
+__global__ __launch_bounds__(kWave) void serve_kernel(ServeArgs sa) {
+    const int lane = (int)threadIdx.x;
+    const uint32_t s = blockIdx.x;
+    char* slot = sa.host + (uint64_t)s * kSrvStride;
+    const uint32_t* seqp = reinterpret_cast<const uint32_t*>(slot);
+    // resume from the last finished request: one posted while no kernel ran is served now
+    uint32_t last = (uint32_t)rdlane((int)(lane == 0 ? sys_load(&reinterpret_cast<const ServeHdr*>(slot)->done) : 0u), 0);
+    uint32_t hb_last = 0;
+    uint64_t t_hb = wall_clock64();
+    for (;;) {
+        const uint32_t v = lane == 0 ? sys_load(seqp)
+                                     : (lane == 1 ? sys_load(&sa.ctl->stop)
+                                                  : (lane == 2 ? sys_load(&sa.ctl->heartbeat) : 0u));
+        const uint32_t seq = (uint32_t)rdlane((int)v, 0), stop = (uint32_t)rdlane((int)v, 1),
+                       hb = (uint32_t)rdlane((int)v, 2);
+        if (seq != last) {
+            serve_one<MODE>(sa, s, slot, seq, lane);
+            last = seq;
+            t_hb = wall_clock64();
+            continue;
+        }
+        if (stop) break;
+        const uint64_t now = wall_clock64();
+        if (hb != hb_last) {
+            hb_last = hb;
+            t_hb = now;
+        } else if (now - t_hb > sa.hb_timeout) {
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+}
+#endif  // TA_FILL_CIGAR
 
 #endif  // TA_FILL_MODE
 
@@ -461,6 +562,13 @@ hipError_t launch_fill_mode<TA_FILL_MODE, (TA_FILL_CIGAR != 0)>(bool wide, const
     else hipLaunchKernelGGL((fill_kernel<MODE, CIGAR, false>), g, b, 0, s, a);
     return hipGetLastError();
 }
+#if TA_FILL_CIGAR
+template <>
+hipError_t launch_serve_mode<TA_FILL_MODE>(const ServeArgs& a, uint32_t slots, hipStream_t s) {
+    hipLaunchKernelGGL(serve_kernel<TA_FILL_MODE>, dim3(slots), dim3(kWave), 0, s, a);
+    return hipGetLastError();
+}
+#endif
 #endif
 
 #ifdef TA_TU_MISC
@@ -534,6 +642,15 @@ extern "C" int ta_lw_prof(unsigned long long* out, int reset) {
     return 0;
 }
 #endif
+
+hipError_t launch_serve(int mode, const ServeArgs& a, uint32_t slots, hipStream_t s) {
+    switch (mode) {
+        case kGlobal: return launch_serve_mode<kGlobal>(a, slots, s);
+        case kLocal: return launch_serve_mode<kLocal>(a, slots, s);
+        case kSemi: return launch_serve_mode<kSemi>(a, slots, s);
+        default: return hipErrorInvalidValue;
+    }
+}
 
 hipError_t launch_compact(const CompactArgs& a, hipStream_t s) {
     if (!a.n_pairs) return hipSuccess;

@@ -64,15 +64,13 @@ constexpr int kLwQEnt = kLwStripes * kRows;            // 128 query rows (u16: b
 constexpr int kLwTEnt = kLwSteps + kLwStripes;         // 72 target columns (u16 likewise)
 constexpr int kLwGroupDw = kLwTileDw + kLwQEnt / 2 + kLwTEnt / 2 + 1 + kLwRunCap + 7;  // +7: group bases on different banks
 
-typedef uint32_t lw_u32x4 __attribute__((ext_vector_type(4)));  // native vector (uint4's union blocks SROA)
-
 // Staging registers of one tile (per lane: its share of the loads).
 template <int G>
 struct LwStage {
     static constexpr int NL = 2 * kLwSteps / G;       // 16-byte pieces of codes
     static constexpr int NQ = kLwQEnt / G;            // query bytes
     static constexpr int NT = (kLwTEnt + G - 1) / G;  // target bytes
-    lw_u32x4 v[NL];
+    uint4 v[NL];
     uint32_t q[NQ], t[NT];
 };
 
@@ -84,29 +82,6 @@ struct LwStage {
 // [0, 71], its step lc + (lr >> 4) - 7.  Every load comes from a clamped
 // (valid) address, so a stage costs one memory latency.  All G lanes of the
 // group.
-// The loads of the tile of pass tP, stripes [L0, L0 + 8), steps [T0, T0 + 64);
-// its first row and column: rowbase, cb.
-template <int G>
-__device__ __forceinline__ void lw_issue_tile(uint32_t tP, uint32_t L0, uint32_t T0, int& rowbase, int& cb,
-                                              LwStage<G>& st, const uint32_t* P, const uint8_t* Q, const uint8_t* T,
-                                              uint32_t n, uint32_t m, uint32_t li) {
-    const uint32_t Tmax = pass_steps(m);
-    rowbase = (int)(tP * (uint32_t)kPassRows + L0 * (uint32_t)kRows);
-    cb = (int)T0 - (int)L0 - (kLwStripes - 1);
-    // one 64-bit base per stage, 32-bit dword offsets per load (full-rate math)
-    const uint32_t* Pp = P + ((uint64_t)tP * Tmax * kWave + L0);
-#pragma unroll
-    for (int k = 0; k < LwStage<G>::NL; ++k) {
-        const uint32_t x = li + (uint32_t)G * k, ts = min(T0 + (x >> 1), Tmax - 1u);
-        st.v[k] = *(const lw_u32x4*)(Pp + (ts * (uint32_t)kWave + 4u * (x & 1u)));
-    }
-#pragma unroll
-    for (int k = 0; k < LwStage<G>::NQ; ++k) st.q[k] = Q[min((uint32_t)rowbase + li + (uint32_t)G * k, n - 1u)];
-#pragma unroll
-    for (int k = 0; k < LwStage<G>::NT; ++k)
-        st.t[k] = T[(uint32_t)min(max(cb + (int)(li + (uint32_t)G * k), 0), (int)m - 1)];
-}
-
 template <int G>
 __device__ __forceinline__ void lw_issue(int row, int col, int& rowbase, int& cb, int& lr, int& lc, uint32_t& T0,
                                          LwStage<G>& st, const uint32_t* P, const uint8_t* Q, const uint8_t* T,
@@ -114,27 +89,24 @@ __device__ __forceinline__ void lw_issue(int row, int col, int& rowbase, int& cb
     const uint32_t ln = ((uint32_t)row >> 4) & 63u, tP = (uint32_t)row >> 10;
     const uint32_t t = (uint32_t)col + ln;
     const uint32_t L0 = (max(ln, 4u) - 4u) & ~3u;
+    const uint32_t Tmax = pass_steps(m);
     T0 = max(t, (uint32_t)kLwSteps - 1u) - (uint32_t)(kLwSteps - 1);
-    lw_issue_tile<G>(tP, L0, T0, rowbase, cb, st, P, Q, T, n, m, li);
+    rowbase = (int)(tP * (uint32_t)kPassRows + L0 * (uint32_t)kRows);
+    cb = (int)T0 - (int)L0 - (kLwStripes - 1);
     lr = row - rowbase;
     lc = col - cb;
-}
-
-// The tile the walk most likely enters after the one at (rowbase, T0): the 64
-// steps to its left, 4 stripes (64 rows) higher -- where a diagonal path that
-// entered at the tile's bottom right leaves it (~60 cells up and left).  Its
-// loads are issued when the walk enters the current tile and land while it
-// walks (~60 dependent LDS round trips); a path that leaves elsewhere (a long D
-// run through the top) stages its tile on the spot.
-template <int G>
-__device__ __forceinline__ bool lw_prefetch(int rowbase, uint32_t T0, int& nrb, int& ncb, uint32_t& nT0,
-                                            LwStage<G>& nx, const uint32_t* P, const uint8_t* Q, const uint8_t* T,
-                                            uint32_t n, uint32_t m, uint32_t li) {
-    if (T0 == 0u) return false;  // the walk cannot leave to the left
-    const uint32_t tP = (uint32_t)rowbase >> 10, L0 = ((uint32_t)rowbase >> 4) & 63u;
-    nT0 = max(T0, (uint32_t)kLwSteps) - (uint32_t)kLwSteps;
-    lw_issue_tile<G>(tP, max(L0, 4u) - 4u, nT0, nrb, ncb, nx, P, Q, T, n, m, li);
-    return true;
+    // one 64-bit base per stage, 32-bit dword offsets per load (full-rate math)
+    const uint32_t* Pp = P + ((uint64_t)tP * Tmax * kWave + L0);
+#pragma unroll
+    for (int k = 0; k < LwStage<G>::NL; ++k) {
+        const uint32_t x = li + (uint32_t)G * k, ts = min(T0 + (x >> 1), Tmax - 1u);
+        st.v[k] = *(const uint4*)(Pp + (ts * (uint32_t)kWave + 4u * (x & 1u)));
+    }
+#pragma unroll
+    for (int k = 0; k < LwStage<G>::NQ; ++k) st.q[k] = Q[min((uint32_t)rowbase + li + (uint32_t)G * k, n - 1u)];
+#pragma unroll
+    for (int k = 0; k < LwStage<G>::NT; ++k)
+        st.t[k] = T[(uint32_t)min(max(cb + (int)(li + (uint32_t)G * k), 0), (int)m - 1)];
 }
 
 // Write a staged tile into the group's LDS: codes ([step][stripe] dwords),
@@ -146,7 +118,7 @@ __device__ __forceinline__ void lw_commit(const LwStage<G>& st, uint32_t* tile, 
                                           uint32_t li) {
     const uint32_t gq = (uint32_t)gap & 0xFFu;
 #pragma unroll
-    for (int k = 0; k < LwStage<G>::NL; ++k) *(lw_u32x4*)(tile + 4u * (li + (uint32_t)G * k)) = st.v[k];
+    for (int k = 0; k < LwStage<G>::NL; ++k) *(uint4*)(tile + 4u * (li + (uint32_t)G * k)) = st.v[k];
 #pragma unroll
     for (int k = 0; k < LwStage<G>::NQ; ++k) {
         const uint32_t c = st.q[k];
@@ -244,10 +216,7 @@ __device__ __forceinline__ void traceback_lane_local(const TraceArgs& a, uint32_
     bool live = has && H > 0;           // a positive score has its goal at i, j >= 1
     bool stage = live;                  // needs a tile around (row, col)
     int row = (int)gi - 1, col = (int)gj - 1;
-    LwStage<G> st, nx;          // the tile being staged; the prefetched next tile
-    int nrb = 0, ncb = 0;        // the prefetched tile's first row and column
-    uint32_t nT0 = 0;
-    bool npf = false;            // nx holds loads of the predicted next tile
+    LwStage<G> st;
 #ifdef TA_LW_PROF
     uint64_t lwp[5] = {0, 0, 0, 0, 0};
 #endif
@@ -259,26 +228,8 @@ __device__ __forceinline__ void traceback_lane_local(const TraceArgs& a, uint32_
                 if (row < 0 || col < 0) {
                     live = false;  // (cannot happen: the cost of row / column 0 is 0)
                 } else {
-                    const int lrB = row - nrb, lcB = col - ncb, sB = lcB + (lrB >> 4) - (kLwStripes - 1);
-                    if (npf && lrB >= 0 && lrB < kLwStripes * kRows && sB >= 0 && sB < kLwSteps) {
-                        // the walk entered the prefetched tile: element copies (a struct copy or a
-                        // second commit call makes the compiler keep both stages in scratch)
-#pragma unroll
-                        for (int k = 0; k < LwStage<G>::NL; ++k) st.v[k] = nx.v[k];
-#pragma unroll
-                        for (int k = 0; k < LwStage<G>::NQ; ++k) st.q[k] = nx.q[k];
-#pragma unroll
-                        for (int k = 0; k < LwStage<G>::NT; ++k) st.t[k] = nx.t[k];
-                        rowbase = nrb;
-                        cb = ncb;
-                        T0 = nT0;
-                        lr = lrB;
-                        lc = lcB;
-                    } else {
-                        lw_issue<G>(row, col, rowbase, cb, lr, lc, T0, st, P, Q, T, n, m, li);
-                    }
+                    lw_issue<G>(row, col, rowbase, cb, lr, lc, T0, st, P, Q, T, n, m, li);
                     lw_commit<G>(st, tile, qw, tw, gap, li);
-                    npf = lw_prefetch<G>(rowbase, T0, nrb, ncb, nT0, nx, P, Q, T, n, m, li);
                 }
                 stage = false;
             }

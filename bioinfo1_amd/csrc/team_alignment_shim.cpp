@@ -8,9 +8,14 @@
 // kernels; there is no CPU fallback.  Error behaviour mirrors the reference:
 // std::invalid_argument with the same two messages; a missing or failing GPU
 // raises std::runtime_error (the mapper's catch (std::exception&) at
-// team_mapper.cpp:680-683 handles both).
+// team_mapper.cpp:680-683 handles both).  The GPU a call runs on:
+// ta_set_default_device, else TEAM_ALIGN_DEVICE, else the calling thread's
+// current HIP device.
 //
-// Concurrent calls are combined: the mapper calls Align once per read from
+// A pair that fits (n <= 4096, m <= 16384) goes to a resident single-pair
+// server (ta_server.cpp): no launch and no copy per call.  Others, or every
+// call with TEAM_ALIGN_SERVER=0, take the batch path:
+// concurrent calls are combined: the mapper calls Align once per read from
 // OpenMP threads (team_mapper.cpp:596), and one pair cannot fill a GPU.  A
 // call queues its pair; if no batch is running, the caller becomes the
 // leader: it takes the queued pairs, aligns them as one batch (one upload,
@@ -18,9 +23,12 @@
 // a leader to take its pair.  A lone caller runs its own one-pair
 // batch at once (no added wait), and under load a batch holds every pair
 // that arrived while the previous one ran.
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
+#include <map>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -36,22 +44,50 @@ namespace {
 // pinned upload, the kernels, one download, one synchronisation
 // (ta_host_batch.h).  The host staging vectors are grow-only too.
 struct ThreadCtx {
-    ta_context* ctx = nullptr;
+    std::map<int, ta_context*> ctx;  // per device
     std::vector<char> qbytes, tbytes, arena;
     std::vector<uint64_t> qoff, toff, coff;
     std::vector<uint32_t> qlen, tlen, tb, clen;
     std::vector<int32_t> score;
-    ~ThreadCtx() { ta_context_destroy(ctx); }
+    ~ThreadCtx() {
+        for (auto& kv : ctx) ta_context_destroy(kv.second);
+    }
 };
 
 thread_local ThreadCtx tc;
 
-ta_context* thread_context() {
-    if (!tc.ctx) {
-        int r = ta_context_create(0, &tc.ctx);
-        if (r != TA_OK) throw std::runtime_error("team::Align: no usable gfx950 GPU (" + std::string(ta_status_string(r)) + ")");
+ta_context* thread_context(int device) {
+    ta_context*& c = tc.ctx[device];
+    if (!c) {
+        int r = ta_context_create(device, &c);
+        if (r != TA_OK) {
+            c = nullptr;
+            throw std::runtime_error("team::Align: no usable gfx950 GPU " + std::to_string(device) + " (" +
+                                     std::string(ta_status_string(r)) + ")");
+        }
     }
-    return tc.ctx;
+    return c;
+}
+
+// The device a call runs on: ta_set_default_device's choice, else the
+// TEAM_ALIGN_DEVICE environment variable (read once), else the calling
+// thread's current HIP device (hipSetDevice) -- so a multi-GPU process whose
+// threads each select their GPU gets its calls there.
+std::atomic<int> g_default_device{-1};
+
+int env_device() {
+    static const int d = [] {
+        const char* e = std::getenv("TEAM_ALIGN_DEVICE");
+        return (e && *e) ? std::atoi(e) : -1;
+    }();
+    return d;
+}
+
+int call_device() {
+    int d = g_default_device.load(std::memory_order_relaxed);
+    if (d >= 0) return d;
+    if ((d = env_device()) >= 0) return d;
+    return ta_current_device();
 }
 
 struct Request {
@@ -61,6 +97,7 @@ struct Request {
     uint32_t tl;
     int type, match, mismatch, gap;
     std::string* cigar;
+    int device = 0;
     int32_t score = 0;
     uint32_t target_begin = 0;
     int status = TA_OK;
@@ -69,6 +106,31 @@ struct Request {
     bool taken = false;   // in a running batch
     bool done = false;
 };
+
+// ---- the low-latency path: one process-wide single-pair server per (device,
+// type), created on first use (TEAM_ALIGN_SERVER=0 turns it off: every call
+// then goes through the combined batches below).
+constexpr uint32_t kServerSlots = 32;
+
+bool server_enabled() {
+    static const bool on = [] {
+        const char* e = std::getenv("TEAM_ALIGN_SERVER");
+        return !(e && std::strcmp(e, "0") == 0);
+    }();
+    return on;
+}
+
+ta_server* server_for(int device, int type) {
+    static std::mutex mu;
+    static std::map<std::pair<int, int>, ta_server*> servers;  // nullptr: creation failed, do not retry
+    std::lock_guard<std::mutex> g(mu);
+    auto it = servers.find({device, type});
+    if (it != servers.end()) return it->second;
+    ta_server* s = nullptr;
+    if (ta_server_create(device, type, kServerSlots, &s) != TA_OK) s = nullptr;
+    servers[{device, type}] = s;
+    return s;
+}
 
 // One batch at a time.  A new leader first waits (at most kGather) until as
 // many pairs are queued as its predecessor's batch held: the callers that
@@ -86,11 +148,16 @@ size_t g_last_batch = 1;
 
 bool same_batch(const Request* a, const Request* b) {
     return a->type == b->type && a->match == b->match && a->mismatch == b->mismatch && a->gap == b->gap &&
-           (a->cigar != nullptr) == (b->cigar != nullptr);
+           (a->cigar != nullptr) == (b->cigar != nullptr) && a->device == b->device;
 }
 
-// Align reqs[0..n) (same type, scores and CIGAR request) as one batch.
-void run_batch(Request* const* reqs, size_t n) {
+// Align reqs[0..n) (same type, scores, CIGAR request and device) as one batch.
+// A failed batch of several pairs is rerun pair by pair: one caller's pair
+// (a huge pair the device cannot hold) must not fail the callers it was
+// combined with -- the reference's calls are independent.
+void run_batch(Request* const* reqs, size_t n);
+
+void run_batch_once(Request* const* reqs, size_t n, int& status) {
     ThreadCtx& c = tc;
     c.qoff.resize(n), c.toff.resize(n), c.qlen.resize(n), c.tlen.resize(n);
     c.score.resize(n), c.tb.resize(n), c.coff.resize(n), c.clen.resize(n);
@@ -112,7 +179,7 @@ void run_batch(Request* const* reqs, size_t n) {
     int r = TA_OK;
     std::string err;
     try {
-        ta_context* ctx = thread_context();
+        ta_context* ctx = thread_context(reqs[0]->device);
         // (the default plan also for small batches: packed couples and the lane
         // walk beat one int32 wave per pair with its walk inside the fill from 2
         // pairs up, 200x200: 8 pairs 221 vs 267 us, scripts/exp/batch_latency.py)
@@ -125,6 +192,8 @@ void run_batch(Request* const* reqs, size_t n) {
         r = TA_ERR_DEVICE;
         err = e.what();
     }
+    status = r;
+    if (r != TA_OK && n > 1) return;  // run_batch reruns the pairs one by one
     for (size_t k = 0; k < n; ++k) {
         Request* q = reqs[k];
         q->status = r;
@@ -137,6 +206,13 @@ void run_batch(Request* const* reqs, size_t n) {
         }
         q->filled = true;
     }
+}
+
+void run_batch(Request* const* reqs, size_t n) {
+    int r = TA_OK;
+    run_batch_once(reqs, n, r);
+    if (r != TA_OK && n > 1)
+        for (size_t k = 0; k < n; ++k) run_batch_once(reqs + k, 1, r);
 }
 
 // The leader's work: the taken requests grouped by scoring (in arrival order).
@@ -164,7 +240,27 @@ int Align(const char* query, unsigned int query_len, const char* target, unsigne
     const int t = static_cast<int>(type);
     if (t != TA_GLOBAL && t != TA_LOCAL && t != TA_SEMI_GLOBAL)
         throw std::invalid_argument("Unknown AlignmentType provided.");  // team_alignment.cpp:73
-    Request req{query, query_len, target, target_len, t, match, mismatch, gap, cigar};
+    const int device = call_device();
+    if (server_enabled()) {
+        ta_server* srv = server_for(device, t);
+        if (srv && ta_server_fits(srv, query_len, target_len, match, mismatch, gap)) {
+            thread_local std::vector<char> cbuf;
+            const uint64_t cap = ta_cigar_slot_bytes(query_len, target_len);
+            if (cigar && cbuf.size() < cap) cbuf.resize(cap);
+            int32_t sc = 0;
+            uint32_t tb = 0, cl = 0;
+            const int r = ta_server_align(srv, query, query_len, target, target_len, match, mismatch, gap,
+                                          cigar != nullptr, &sc, &tb, cigar ? cbuf.data() : nullptr, cap, &cl);
+            if (r == TA_OK) {
+                if (cigar) cigar->assign(cbuf.data(), cl);  // assigned, not appended (:160)
+                if (target_begin) *target_begin = tb;
+                return sc;
+            }
+            if (r != TA_ERR_UNSERVED)
+                throw std::runtime_error(std::string("team::Align: ") + ta_status_string(r));
+        }
+    }
+    Request req{query, query_len, target, target_len, t, match, mismatch, gap, cigar, device};
     {
         std::unique_lock<std::mutex> lk(g_mu);
         g_queue.push_back(&req);
@@ -205,3 +301,9 @@ int Align(const char* query, unsigned int query_len, const char* target, unsigne
 }
 
 }  // namespace team
+
+extern "C" int ta_set_default_device(int device) {
+    if (device >= ta_device_count()) return TA_ERR_ARG;
+    g_default_device.store(device < 0 ? -1 : device, std::memory_order_relaxed);
+    return TA_OK;
+}

@@ -44,6 +44,7 @@ cc "$B/ta_misc.o" "$CS/ta_kernels.hip" "$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$
 # affine-gap extension (fill + traceback kernels and its plan driver)
 cc "$B/ta_affine.o" "$CS/ta_affine.hip" "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_affine.hip"
 cc "$B/ta_api.o" "$CS/ta_api.hip" "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_api.hip"
+cc "$B/ta_server.o" "$CS/ta_server.cpp" "$HIPCC" "${FLAGS[@]}" -x hip -c "$CS/ta_server.cpp"
 cc "$B/shim.o" "$CS/team_alignment_shim.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/team_alignment_shim.cpp"
 # host planner: plain C++ (also built with g++ under ASan/UBSan/TSan by tests/test_host_sanitizers.py)
 cc "$B/ta_planner.o" "$CS/ta_planner.cpp" g++ -O2 -std=c++17 -fPIC -Wall -c "$CS/ta_planner.cpp"
@@ -56,7 +57,7 @@ for f in tm_api tm_fastx; do
 done
 cc "$B/tm_main.o" "$CS/tm_main.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp"
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_planner.o" "$B/shim.o" \
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_server.o" "$B/ta_planner.o" "$B/shim.o" \
   -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$OUT"
 PKG="$ROOT/bioinfo1_amd"
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/tm_{minimizers,match,chain,api,fastx}.o -L"$PKG" -lteam_alignment -lz \

@@ -59,11 +59,46 @@ void ta_context_destroy(ta_context* ctx);
  * one).  Waits for the context's last execution.  The context stays usable. */
 void ta_context_release(ta_context* ctx);
 
-/* Device bytes the context currently holds in its grow-only buffers (the
- * code workspace and staging).  A caller sizing ta_plan_create's workspace
- * budget from hipMemGetInfo adds this back: the free figure does not count
- * memory the context will reuse. */
+/* Device bytes the context holds in its grow-only traceback-code and
+ * pass-boundary workspace -- the memory a plan's chunks reuse.  A caller sizing
+ * ta_plan_create's workspace budget from hipMemGetInfo adds this back: the free
+ * figure does not count memory the context will reuse.  (Staging and output
+ * buffers are not included: a plan cannot reuse them.) */
 uint64_t ta_context_held_bytes(const ta_context* ctx);
+
+/* ---- Low-latency single pairs (the drop-in team::Align's path for calls that
+ * fit).  Replaces team::Align's per-call synchronous computation
+ * (team_alignment.cpp:49-56) as called by team_mapper.cpp:666-678 / 755-767:
+ * a persistent kernel (one wave per slot) serves pairs posted in pinned host
+ * memory, so a call costs no kernel launch and no copy.  One server per
+ * (device, alignment type); its kernel starts with the first call and stops
+ * after ~200 ms without calls.  Thread-safe: concurrent callers take
+ * different slots. */
+typedef struct ta_server ta_server;
+int ta_server_create(int device, int type, uint32_t slots, ta_server** out); /* slots 1..64 */
+void ta_server_destroy(ta_server* server);
+/* 1 when an n x m pair with these scores runs on the server (n <= 4096,
+ * m <= 16384; local mode: (n + m) * max|score| < 2^25). */
+int ta_server_fits(const ta_server* server, uint32_t query_len, uint32_t target_len, int match, int mismatch,
+                   int gap);
+/* One pair, synchronous, team::Align's results (score, target_begin, the CIGAR
+ * bytes when want_cigar).  TA_ERR_UNSERVED when the pair does not fit or no
+ * slot is free: use ta_align_batch instead. */
+int ta_server_align(ta_server* server, const char* query, uint32_t query_len, const char* target,
+                    uint32_t target_len, int match, int mismatch, int gap, int want_cigar, int32_t* score,
+                    uint32_t* target_begin, char* cigar, uint64_t cigar_capacity, uint32_t* cigar_len);
+/* 1 while the server's kernel is resident. */
+int ta_server_running(const ta_server* server);
+
+/* The drop-in team::Align (include/team_alignment.hpp) runs each call on:
+ * the device set here (device >= 0; -1 clears the choice), else the device
+ * named by the TEAM_ALIGN_DEVICE environment variable (read once), else the
+ * calling thread's current HIP device (hipSetDevice).  TA_ERR_ARG for a device
+ * that does not exist. */
+int ta_set_default_device(int device);
+/* The calling thread's current HIP device (0 when it has none) and the number of devices. */
+int ta_current_device(void);
+int ta_device_count(void);
 
 /* Bytes of the per-pair CIGAR slot for an n x m pair: 2*(n+m)+2, an upper
  * bound on any run-length CIGAR of that pair (team_alignment.cpp:145-160). */
@@ -192,6 +227,7 @@ int ta_compact_cigars(ta_context* ctx, uint32_t n_pairs, const char* cigar_slots
  * |gap_open| + |gap_extend|) must be < 2^26, else TA_ERR_RANGE.
  */
 #define TA_ERR_RANGE 6 /* affine scoring x lengths outside the int32-safe range */
+#define TA_ERR_UNSERVED 7 /* ta_server_align: the pair is outside the server's limits, or every slot is busy */
 
 typedef struct ta_affine_plan ta_affine_plan;
 

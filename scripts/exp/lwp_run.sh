@@ -1,8 +1,12 @@
 set -u
 cp bioinfo1_amd/libteam_alignment.so build/exp/_orig.so
-cp build/exp/lwprof.so bioinfo1_amd/libteam_alignment.so
-timeout -k 10 200 python -u scripts/exp/lw_prof.py > gpurun_out/lwp.log 2>&1; rc=$?
-timeout -k 10 200 python -u scripts/exp/lw_prof.py --related >> gpurun_out/lwp.log 2>&1
+rc=0
+for v in ${LWP_VARIANTS:-lwprof}; do
+  cp build/exp/$v.so bioinfo1_amd/libteam_alignment.so
+  echo "== $v" >> gpurun_out/lwp.log
+  timeout -k 10 200 python -u scripts/exp/lw_prof.py >> gpurun_out/lwp.log 2>&1 || rc=1
+  timeout -k 10 200 python -u scripts/exp/lw_prof.py --related >> gpurun_out/lwp.log 2>&1 || rc=1
+done
 cp build/exp/_orig.so bioinfo1_amd/libteam_alignment.so
-cat gpurun_out/lwp.log | grep iter
+grep "iter 2\|==" gpurun_out/lwp.log
 exit $rc

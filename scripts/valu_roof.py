@@ -52,6 +52,15 @@ def parse_rates(path):
     return rates
 
 
+# Opcodes measured only in a pair, or whose single-op kernel is not a throughput test:
+#  v_mov_b32      -- "v_mov_b32+v_add_u32 (x2)" averages 2.33 with v_add_u32 at 2.89: ~1.8, class 2
+#  v_readlane_b32 -- its pair kernel chains every lane read through one SGPR (serialised);
+#                    a VOP3 cross-lane read, counted as class 4
+#  v_cndmask_b32  -- the VOP2 form's kernel reads a VCC nothing writes (22.9, an artifact);
+#                    the VOP3 form with an SGPR mask runs 4.30, and the e32 form is counted alike
+DERIVED = {"v_mov_b32": 2.0, "v_readlane_b32": 4.0, "v_cndmask_b32": None}
+
+
 def issue_class(c):
     return min((2, 4, 8, 16), key=lambda k: abs(k - c))
 
@@ -61,14 +70,22 @@ def base_op(op):
     return op
 
 
-def census(src, defines, sym):
-    out = "/tmp/valu_roof"
+def asm_of(src, defines):
+    """gfx950 assembly of a translation unit (cached per source + defines)."""
+    key = src.rsplit(".", 1)[0] + "".join(d.replace("-D", "_").replace("=", "") for d in defines)
+    out = os.path.join("/tmp/valu_roof", key)
     os.makedirs(out, exist_ok=True)
     stem = src.rsplit(".", 1)[0]
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", *defines, "-c",
-                           os.path.join(CS, src), "-o", f"{out}/k.o", "-save-temps"], cwd=out,
-                          stderr=subprocess.DEVNULL)
-    text = open(f"{out}/{stem}-hip-amdgcn-amd-amdhsa-gfx950.s").read()
+    s_file = f"{out}/{stem}-hip-amdgcn-amd-amdhsa-gfx950.s"
+    if not os.path.exists(s_file) or os.path.getmtime(s_file) < os.path.getmtime(os.path.join(CS, src)):
+        subprocess.check_call(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", *defines,
+                               "--cuda-device-only", "-S", os.path.join(CS, src), "-o", s_file], cwd=out,
+                              stderr=subprocess.DEVNULL)
+    return open(s_file).read()
+
+
+def census(src, defines, sym):
+    text = asm_of(src, defines)
     funcs = re.split(r"\n(?=_Z\w+:)", text)
     body = [f for f in funcs if f.split(":")[0].find(sym) >= 0 and "s_endpgm" in f][0].split(".Lfunc_end")[0]
     lines = body.splitlines()
@@ -97,7 +114,11 @@ def roof(mix, rates):
         b = base_op(op)
         if op.endswith("_dpp"):
             b = "v_mov_b32_dpp" if op.startswith("v_mov") else b
-        meas = rates.get(b)
+        meas = rates.get(op)  # an encoding measured on its own (v_cndmask_b32_e64)
+        if meas is None and b in DERIVED:
+            meas = DERIVED[b] if DERIVED[b] is not None else rates.get(b + "_e64")
+        if meas is None:
+            meas = rates.get(b)
         if meas is None and op.endswith("_dpp"):
             meas = rates.get("v_mov_b32_dpp")
         k = issue_class(meas) if meas is not None else (4 if b.startswith("v_pk_") else 2)
@@ -116,8 +137,12 @@ def main():
     rates = parse_rates(a.rates)
     res = {"rates_source": os.path.relpath(a.rates, ROOT), "method": __doc__.split("\n\n")[1].strip(),
            "kernels": {}}
-    for tag, (src, defs, sym) in KERNELS.items():
-        mix = census(src, defs, sym)
+    from concurrent.futures import ThreadPoolExecutor
+
+    with ThreadPoolExecutor(len(KERNELS)) as ex:  # compile the translation units in parallel
+        mixes = dict(zip(KERNELS, ex.map(lambda kv: census(*kv[1]), KERNELS.items())))
+    for tag in KERNELS:
+        mix = mixes[tag]
         mean, per = roof(mix, rates)
         peak = SIMDS * 64 * CLOCK / mean / 1e12
         four = sum(v["count"] for v in per.values() if v["class_cycles"] >= 4) / sum(v["count"] for v in per.values())

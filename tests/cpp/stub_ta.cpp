@@ -39,6 +39,47 @@ int ta_context_create(int device, ta_context** out) {
 
 void ta_context_destroy(ta_context* ctx) { delete ctx; }
 
+int ta_current_device(void) { return 0; }
+int ta_device_count(void) { return 1; }
+
+// The single-pair server: the oracle again, for pairs of even query length
+// (the others take the shim's batch path, so both run under TSan).
+struct ta_server {
+    int type = 0;
+};
+
+int ta_server_create(int device, int type, uint32_t slots, ta_server** out) {
+    (void)device;
+    (void)slots;
+    *out = new ta_server();
+    (*out)->type = type;
+    return TA_OK;
+}
+
+void ta_server_destroy(ta_server* s) { delete s; }
+
+int ta_server_fits(const ta_server* s, uint32_t n, uint32_t m, int match, int mismatch, int gap) {
+    (void)s, (void)m, (void)match, (void)mismatch, (void)gap;
+    return n % 2 == 0;
+}
+
+int ta_server_running(const ta_server* s) { return s != nullptr; }
+
+int ta_server_align(ta_server* s, const char* q, uint32_t n, const char* t, uint32_t m, int match, int mismatch,
+                    int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* cigar, uint64_t cigar_cap,
+                    uint32_t* cigar_len) {
+    int sc = 0;
+    unsigned b = 0;
+    size_t cl = 0;
+    const int r = oracle_align(q, n, t, m, s->type, match, mismatch, gap, want_cigar, &sc, &b,
+                               want_cigar ? cigar : nullptr, want_cigar ? cigar_cap : 0, &cl);
+    if (r) return r;
+    *score = sc;
+    *target_begin = b;
+    if (want_cigar) *cigar_len = (uint32_t)cl;
+    return TA_OK;
+}
+
 uint64_t ta_cigar_slot_bytes(uint32_t n, uint32_t m) { return 2ull * ((uint64_t)n + m) + 2; }
 
 int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint64_t* qoff, const uint32_t* qlen,

@@ -639,3 +639,59 @@ def test_self_coupled_single_pair_with_dash(aligner, oracle, mode):
             got = aligner.align_batch(b, mode, 1, -1, -1, True)
             assert (int(got.scores[0]), int(got.target_begins[0]), got.cigar(0)) == (
                 int(want.scores[0]), int(want.target_begins[0]), want.cigar(0)), where
+
+
+def test_single_pair_server(kat_cases, random_cases, oracle):
+    """The resident single-pair server (ta_server_*, the drop-in's path for
+    pairs that fit): every KAT and random case of its mode, score-only too;
+    multi-pass pairs (n > 1024); calls from 8 threads at once; a pause past
+    the idle stop, after which the next call relaunches the kernel."""
+    import threading
+    import time
+
+    from bioinfo1_amd.align import Server
+
+    cases = [c for c in kat_cases + random_cases if not c["error"]]
+    for mode in (0, 1, 2):
+        srv = Server(0, mode)
+        try:
+            for c in (c for c in cases if c["type"] == mode):
+                q, t = bytes.fromhex(c["query"]), bytes.fromhex(c["target"])
+                args = (c["match"], c["mismatch"], c["gap"])
+                if not srv.fits(len(q), len(t), *args):
+                    continue
+                got = srv.align(q, t, *args)
+                assert got == (c["score"], bytes.fromhex(c["cigar"]), c["target_begin"]), (c["source"], got)
+                assert srv.align(q, t, *args, want_cigar=False) == (c["score"], None, c["target_begin"])
+            b = synth.related_batch(6, 2500, 2300, seed=91 + mode)  # 3 passes
+            want = oracle.align_batch(b, mode, 1, -1, -1, True)
+            for p in range(b.n_pairs):
+                assert srv.align(b.query(p), b.target(p), 1, -1, -1) == (
+                    int(want.scores[p]), want.cigar(p), int(want.target_begins[p]))
+            rb = synth.ragged_batch(160, 0, 600, seed=0x7E + mode, alphabet=b"ACGT-N")
+            rw = oracle.align_batch(rb, mode, 2, -1, -1, True)
+            errs = []
+
+            def worker(k):
+                for p in range(k, rb.n_pairs, 8):
+                    got = srv.align(rb.query(p), rb.target(p), 2, -1, -1)
+                    if got != (int(rw.scores[p]), rw.cigar(p), int(rw.target_begins[p])):
+                        errs.append(p)
+
+            th = [threading.Thread(target=worker, args=(k,)) for k in range(8)]
+            for x in th:
+                x.start()
+            for x in th:
+                x.join()
+            assert not errs, errs[:5]
+            time.sleep(0.5)  # past the idle stop (200 ms): the kernel has ended
+            assert not srv.running()
+            assert srv.align(b"GTACC", b"GATACGTTA", 1, -1, -1)[0] == want_score_cfg1(mode)
+            assert srv.running()
+            assert not srv.fits(5000, 10, 1, -1, -1) and not srv.fits(10, 20000, 1, -1, -1)
+        finally:
+            srv.close()
+
+
+def want_score_cfg1(mode):
+    return {0: -1, 1: 3, 2: 2}[mode]  # SURVEY §4 table 2, GTACC / GATACGTTA
