@@ -701,7 +701,8 @@ def main_align(args, D):
         if gathered is not None:
             extra["gather"] = check_gathered(args, gathered, plan, full, al, mode, sc, cigar)
         if D.world == 1 and not args.no_host and args.workload == "cfg2" and not affine:
-            extra["host_to_host"] = host_to_host(HostBatchRunner(al, batch, mode, *sc, cigar), batch, args)
+            extra["host_to_host"] = host_to_host_pipelined(al, batch, mode, sc, cigar, args, budget)
+            extra["host_to_host_single_call"] = host_to_host(HostBatchRunner(al, batch, mode, *sc, cigar), batch, args)
         if D.world == 1 and args.workload == "cfg2" and cigar and not affine and not args.no_score_only:
             extra["score_only"] = score_only(al, batch, mode, sc, args, budget, stream)
         if args.check_all and cigar:
@@ -833,6 +834,35 @@ def host_to_host(runner, batch, args, reps=10):
                                      "(CIGARs compacted on the device)", "parity": par}
 
 
+def host_to_host_pipelined(al, batch, mode, sc, cigar, args, budget, reps=10):
+    """SURVEY §8d's GCUPS with the PCIe transfers overlapped (align.HostPipeline):
+    every step uploads the batch from pinned host memory, runs the kernels and
+    downloads every record and the compacted CIGAR bytes into pinned host memory;
+    step k's upload and step k-1's download run beside the kernels."""
+    from bioinfo1_amd.align import HostPipeline
+
+    hp = HostPipeline(al, batch, mode, *sc, cigar, workspace_budget=budget)
+    for _ in range(2):
+        hp.step()
+    hp.drain()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        hp.step()
+    hp.drain()
+    dt = (time.perf_counter() - t0) / reps
+    r = hp.results()
+    hp.close()
+    name, k = digest_name(args, batch.n_pairs)
+    par = parity_vs_digest(r.scores, r.target_begins, r.cigar_lens, r.cigar, name, k) if (name and r.cigar_lens is not None) else None
+    up = batch.qbytes.nbytes + batch.tbytes.nbytes
+    down = 12 * batch.n_pairs + (int(r.cigar_lens.sum()) if r.cigar_lens is not None else 0)
+    return {"value": round(batch.cells / dt / 1e9, 2), "unit": "GCUPS", "ms_per_batch": round(dt * 1e3, 4),
+            "batches": reps, "pcie_bytes_per_batch": {"host_to_device": up, "device_to_host": down},
+            "path": "align.HostPipeline: pinned host bytes -> H2D (upload stream) -> kernels + device CIGAR "
+                    "compaction (compute stream) -> records + exact CIGAR bytes D2H (download stream), two "
+                    "plans alternating", "parity": par}
+
+
 def workload_name(args, cigar, n_pairs, full):
     tail = f"{args.mode}, scoring {args.scoring}, CIGAR {'on' if cigar else 'off'}"
     if args.workload == "cfg3":
@@ -854,21 +884,24 @@ def main_dropin(args):
     """Single-call team::Align (the reference mapper's calling pattern) through
     our drop-in library vs the reference's own Align, same harness, same pairs."""
     res = {}
-    for name, exe in (("amd", os.path.join(ROOT, "build", "dropin_amd")),
-                      ("reference", os.path.join(ROOT, "oracle", "_ref", "dropin_ref"))):
+    # amd: the drop-in as shipped (pairs up to 4096 x 16384 on the resident single-pair server);
+    # amd_batch_path: the same library with TEAM_ALIGN_SERVER=0 (concurrent calls combined into batches)
+    for name, exe, env in (("amd", os.path.join(ROOT, "build", "dropin_amd"), {}),
+                           ("amd_batch_path", os.path.join(ROOT, "build", "dropin_amd"), {"TEAM_ALIGN_SERVER": "0"}),
+                           ("reference", os.path.join(ROOT, "oracle", "_ref", "dropin_ref"), {})):
         if not os.path.exists(exe):
             continue
         rows = []
         for thr in (1, 8, 16):  # 16: the host cores a GPU box grants this job
             p = subprocess.run([exe, str(thr), "1.0", "5x9,200x200,1000x1000", str(MODES[args.mode or "local"])],
-                               capture_output=True, text=True, timeout=300, check=True)
+                               capture_output=True, text=True, timeout=300, check=True, env=dict(os.environ, **env))
             rows += [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
         res[name] = rows
     same = None
     if "amd" in res and "reference" in res:
         key = lambda r: (r["shape"], r["threads"])  # noqa: E731
         ref = {key(r): r["score_checksum"] for r in res["reference"]}
-        same = all(ref.get(key(r)) == r["score_checksum"] for r in res["amd"])
+        same = all(ref.get(key(r)) == r["score_checksum"] for v in ("amd", "amd_batch_path") for r in res.get(v, []))
     print(json.dumps({"metric": "team::Align single-call throughput (drop-in, one pair per call)", "unit": "calls/s",
                       "mode": args.mode or "local", "score_checksums_equal": same, "results": res}), flush=True)
 

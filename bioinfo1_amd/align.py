@@ -125,6 +125,7 @@ def lib() -> C.CDLL:
     L.ta_server_destroy.restype = None
     L.ta_server_fits.argtypes = [C.c_void_p, C.c_uint32, C.c_uint32, C.c_int, C.c_int, C.c_int]
     L.ta_server_running.argtypes = [C.c_void_p]
+    L.ta_server_last_times.argtypes = [C.c_void_p, C.c_uint32, C.POINTER(C.c_double)]
     L.ta_server_align.argtypes = [C.c_void_p, C.c_char_p, C.c_uint32, C.c_char_p, C.c_uint32, C.c_int, C.c_int,
                                   C.c_int, C.c_int, C.POINTER(C.c_int32), C.POINTER(C.c_uint32), C.c_void_p,
                                   C.c_uint64, C.POINTER(C.c_uint32)]
@@ -143,6 +144,7 @@ ABI_SYMBOLS = [
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
     "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
     "ta_server_create", "ta_server_destroy", "ta_server_fits", "ta_server_align", "ta_server_running",
+    "ta_server_last_times",
 ]
 # The drop-in C++ entry point (team_alignment.hpp), g++/libstdc++ cxx11 mangling.
 TEAM_ALIGN_SYMBOL = ("_ZN4team5AlignEPKcjS1_jNS_13AlignmentTypeEiiiPNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEEPj")
@@ -307,6 +309,15 @@ class Server:
     def running(self) -> bool:
         return bool(lib().ta_server_running(self._h))
 
+    def last_times(self, slot: int = 0):
+        """Device phase times (us) of slot's last request: request + bytes to HBM,
+        fill + walk, results out, system fence."""
+        out = (C.c_double * 4)()
+        r = lib().ta_server_last_times(self._h, slot, out)
+        if r != TA_OK:
+            _raise(r)
+        return list(out)
+
     def align(self, query: bytes, target: bytes, match: int, mismatch: int, gap: int, want_cigar: bool = True):
         query, target = bytes(query), bytes(target)
         cap = 2 * (len(query) + len(target)) + 2
@@ -358,12 +369,14 @@ class DevicePlan:
     current torch stream (asynchronous)."""
 
     def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, device=None,
-                 workspace_budget: int = 0, gap_open=None, flags: int = 0, inputs=None):
+                 workspace_budget: int = 0, gap_open=None, flags: int = 0, inputs=None, records=None):
         """gap_open=None: team::Align's linear gap.  gap_open=o: the affine-gap
         extension (ta_affine_plan_*) with gap_extend = gap.  flags: TA_PLAN_*
         kernel selection (tests / measurements; same results).  inputs: the
         batch already in HBM as (query bytes, query offsets, target bytes,
-        target offsets) tensors -- then only batch.qlen / batch.tlen are read."""
+        target offsets) tensors -- then only batch.qlen / batch.tlen are read.
+        records: an int32 device tensor of >= 3 * P entries that receives the
+        scores, target_begins and CIGAR lengths back to back (one download)."""
         import torch
 
         L = lib()
@@ -392,13 +405,18 @@ class DevicePlan:
             self.toff = f(batch.toff.view(np.int64))
         else:
             self.qbytes, self.qoff, self.tbytes, self.toff = inputs
-        self.score = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
-        self.target_begin = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
+        if records is not None:
+            assert records.dtype == torch.int32 and records.numel() >= 3 * self.P and records.is_contiguous()
+            self.score, self.target_begin = records[:self.P], records[self.P:2 * self.P]
+        else:
+            self.score = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
+            self.target_begin = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
         self.slots_bytes = int(self._fn("ta_plan_cigar_slots_bytes")(h))
         self.slots = torch.zeros(max(self.slots_bytes, 1) if self.want_cigar else 1, dtype=torch.uint8,
                                  device=self.dev)
         self.cigar_start = torch.zeros(self.P, dtype=torch.int64, device=self.dev)
-        self.cigar_len = torch.zeros(self.P, dtype=torch.int32, device=self.dev)
+        self.cigar_len = (records[2 * self.P:3 * self.P] if records is not None
+                          else torch.zeros(self.P, dtype=torch.int32, device=self.dev))
         self.io = _DeviceIO(self.qbytes.data_ptr(), self.qoff.data_ptr(), self.tbytes.data_ptr(),
                             self.toff.data_ptr(), self.score.data_ptr(), self.target_begin.data_ptr(),
                             self.slots.data_ptr(), self.cigar_start.data_ptr(), self.cigar_len.data_ptr())
@@ -547,3 +565,123 @@ class HostBatchRunner:
         if not self.want_cigar:
             return BatchResult(self.score.copy(), self.tbeg.copy(), None, None, None)
         return BatchResult(self.score.copy(), self.tbeg.copy(), self.coff.copy(), self.clen.copy(), self.arena.copy())
+
+
+class HostPipeline:
+    """Host-resident batches aligned back to back with the PCIe transfers hidden:
+    batch k's upload runs on an upload stream and batch k-1's download on a
+    download stream while the kernels run on the compute stream.  Inputs are the
+    batch's bytes in pinned host memory; every step uploads them, runs the plan,
+    compacts the CIGARs on the device and brings the records and the compacted
+    CIGAR bytes back into pinned host memory (host inputs to host
+    results).
+
+    Two DevicePlans alternate (double-buffered device inputs and outputs); they
+    share the aligner's context, so their kernels run one after the other.  Step
+    k enqueues its upload and kernels, then waits for step k-1's records (12
+    bytes per pair; step k-1's kernels are done, step k's already queued behind
+    them) and posts the download of exactly step k-1's CIGAR bytes, ahead of
+    step k's records."""
+
+    def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, workspace_budget=0):
+        import torch
+
+        self.torch = torch
+        self.P = P = batch.n_pairs
+        self.want_cigar = bool(want_cigar)
+        dev = torch.device("cuda", aligner.device)
+        self.dev = dev
+        qb = batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8)
+        tb = batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8)
+        self.h_q = torch.from_numpy(np.ascontiguousarray(qb)).pin_memory()
+        self.h_t = torch.from_numpy(np.ascontiguousarray(tb)).pin_memory()
+        qoff = torch.from_numpy(batch.qoff.view(np.int64).copy()).to(dev)
+        toff = torch.from_numpy(batch.toff.view(np.int64).copy()).to(dev)
+        self.d_q = [torch.empty_like(self.h_q, device=dev) for _ in range(2)]
+        self.d_t = [torch.empty_like(self.h_t, device=dev) for _ in range(2)]
+        # per slot: scores, target_begins, CIGAR lengths (written there by the plan) + the CIGAR byte total
+        self.d_rec = [torch.zeros(3 * P + 1, dtype=torch.int32, device=dev) for _ in range(2)]
+        self.plans = [DevicePlan(aligner, batch, type, match, mismatch, gap, want_cigar,
+                                 workspace_budget=workspace_budget, inputs=(self.d_q[i], qoff, self.d_t[i], toff),
+                                 records=self.d_rec[i])
+                      for i in range(2)]
+        self.compute, self.up, self.down = (torch.cuda.Stream(dev) for _ in range(3))
+        self.h_rec = [torch.empty(3 * P + 1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
+        cap = max(self.plans[0].slots_bytes, 1)
+        self.h_cig = [torch.empty(cap, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
+        E = lambda: [torch.cuda.Event() for _ in range(2)]  # noqa: E731
+        self.ev_in, self.ev_done, self.ev_rec, self.ev_cig = E(), E(), E(), E()
+        self.used = [False, False]  # slot has a step in flight (its downloads may still run)
+        self.prev = None            # (slot, device CIGAR bytes) of the previous step
+        self.last = None
+        self.k = 0
+
+    def _download_cigars(self, i, dst):
+        torch = self.torch
+        if self.want_cigar:
+            self.ev_rec[i].synchronize()  # step's records are in (its kernels are done)
+            nbytes = int(self.h_rec[i][3 * self.P])
+            with torch.cuda.stream(self.down):
+                if nbytes:
+                    self.h_cig[i][:nbytes].copy_(dst[:nbytes], non_blocking=True)
+                self.ev_cig[i].record(self.down)
+        else:
+            self.ev_cig[i] = self.ev_rec[i]
+        self.last = i
+
+    def step(self):
+        torch, P = self.torch, self.P
+        i = self.k % 2
+        self.k += 1
+        if self.used[i]:
+            self.ev_cig[i].synchronize()  # slot i's host buffers of two steps ago are filled
+        with torch.cuda.stream(self.up):
+            self.up.wait_event(self.ev_done[i])  # kernels of two steps ago no longer read these inputs
+            self.d_q[i].copy_(self.h_q, non_blocking=True)
+            self.d_t[i].copy_(self.h_t, non_blocking=True)
+            self.ev_in[i].record(self.up)
+        plan = self.plans[i]
+        with torch.cuda.stream(self.compute):
+            self.compute.wait_event(self.ev_in[i])
+            self.compute.wait_event(self.ev_rec[i])  # (the slot's records of two steps ago are down)
+            plan.run()
+            rec = self.d_rec[i]
+            dst = None
+            if self.want_cigar:
+                dst, off = plan.compact_cigars()
+                rec[3 * P:].copy_(off[-1:], non_blocking=True)
+            self.ev_done[i].record(self.compute)
+        if dst is not None:
+            dst.record_stream(self.down)
+        self.used[i] = True
+        if self.prev is not None:  # the previous step's CIGAR bytes, ahead of this step's records
+            self._download_cigars(*self.prev)
+        with torch.cuda.stream(self.down):
+            self.down.wait_event(self.ev_done[i])
+            self.h_rec[i].copy_(rec, non_blocking=True)
+            self.ev_rec[i].record(self.down)
+        self.prev = (i, dst)
+
+    def drain(self):
+        if self.prev is not None:
+            self._download_cigars(*self.prev)
+            self.prev = None
+        self.torch.cuda.synchronize(self.dev)
+
+    def results(self) -> BatchResult:
+        """The last drained step's results (host copies)."""
+        i, P = self.last, self.P
+        rec = self.h_rec[i].numpy()
+        sc = rec[:P].copy()
+        tb = rec[P:2 * P].copy().view(np.uint32)
+        if not self.want_cigar:
+            return BatchResult(sc, tb, None, None, None)
+        ln = rec[2 * P:3 * P].copy().view(np.uint32)
+        off = np.zeros(P, np.uint64)
+        if P:
+            off[1:] = np.cumsum(ln[:-1], dtype=np.uint64)
+        return BatchResult(sc, tb, off, ln, self.h_cig[i].numpy()[:int(rec[3 * P])].copy())
+
+    def close(self):
+        for p in self.plans:
+            p.close()

@@ -350,7 +350,7 @@ __global__ __launch_bounds__(kBlock) void affine_fill_kernel(AffArgs a) {
             best_j = o.row_j;
         }
         if (MODE == kGlobal && last_pass) corner = o.corner;
-        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // boundary row -> next pass
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // boundary row -> next pass
     }
     if (lane == 0) {
         a.score[p] = (MODE == kGlobal) ? corner : best_h;
@@ -783,7 +783,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
             }
             if (MODE == kGlobal && last_pass) corner[h] = o[h].corner;
         }
-        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");  // boundary row -> next pass
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // boundary row -> next pass
     }
     if (lane == 0) {
 #pragma unroll

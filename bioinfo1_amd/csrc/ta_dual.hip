@@ -422,11 +422,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
             }
             if (MODE == kGlobal && last_pass) corner[h] = o.o[h].corner;
         }
-        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
     if (CIGAR && a.fused) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {

@@ -113,7 +113,7 @@ struct ServeHdr {           // the first 128 bytes of a host slot
     uint32_t done;           // device: seq of the last finished request (written last)
     int32_t score;
     uint32_t target_begin, cigar_len, status;
-    uint32_t pad1[11];
+    uint32_t pad1[11];       // [0..3]: the last request's phase clocks (ta_server_last_times)
 };
 static_assert(sizeof(ServeHdr) == kSrvQOff, "ServeHdr layout");
 

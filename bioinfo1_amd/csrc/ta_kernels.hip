@@ -34,41 +34,32 @@ namespace ta {
 namespace {
 
 #ifdef TA_FILL_MODE
-template <int MODE>
-__device__ __forceinline__ void fused_traceback(const FillArgs& a, uint32_t p, const uint32_t* ptrs, uint32_t n,
-                                                uint32_t m, uint32_t gi, uint32_t gj, int lane, int h) {
-    uint64_t st;
-    uint32_t len;
-    const WalkSeq seq{a.qbytes + a.qoff[p], a.tbytes + a.toff[p], h, a.match, a.mismatch, a.gap};
-    traceback_pair<MODE>(ptrs, n, m, gi, gj, a.slots + a.slot_off[p], cigar_slot_bytes(n, m), lane, &st, &len, seq);
-    if (lane == 0) {
-        a.cigar_start[p] = a.slot_off[p] + st;
-        a.cigar_len[p] = len;
-    }
-}
+// A pair's results, wave-uniform: score, target_begin, goal cell and (walked)
+// its CIGAR's first byte in the pair's slot and its length.
+struct PairOut {
+    int score;
+    uint32_t tb, gi, gj;
+    uint64_t cstart;
+    uint32_t clen;
+};
 
 // Degenerate pairs (an empty query or target): closed forms of what the
 // reference computes when one of its loops is empty.
 template <int MODE>
-__device__ void degenerate(const FillArgs& a, uint32_t p, uint32_t n, uint32_t m) {
-    int score = 0;
-    uint32_t gi = 0, gj = 0, tb = 0;
+__device__ __forceinline__ PairOut degenerate(int gap, uint32_t n, uint32_t m) {
+    PairOut o{0, 0, 0, 0, 0, 0};
     if (MODE == kGlobal) {  // :117-121 goal (n,m); boundary cost (n or m)*gap
-        gi = n;
-        gj = m;
-        score = n ? wmul(n, a.gap) : wmul(m, a.gap);
+        o.gi = n;
+        o.gj = m;
+        o.score = n ? wmul(n, gap) : wmul(m, gap);
     } else if (MODE == kLocal) {  // max never set: goal (0,0), tb = 0+1
-        tb = 1;
+        o.tb = 1;
     } else {  // :265-278: (0,m) wins the column scan (cost 0); row scan never beats it
-        gi = 0;
-        gj = (n == 0) ? m : 0;
+        o.gi = 0;
+        o.gj = (n == 0) ? m : 0;
     }
-    a.score[p] = score;
-    a.target_begin[p] = tb;
-    a.goal_i[p] = gi;
-    a.goal_j[p] = gj;
+    return o;
 }
-
 
 // One pass = rows row_base+1 .. row_base+nrows of the query against the whole
 // target.  Compile-time specialisation:
@@ -328,25 +319,25 @@ __device__ __forceinline__ PassOut run_pass_any(const FillArgs& a, const uint8_t
     return run_pass_nv<MODE, CIGAR, WIDE, false>(a, Q, T, n, m, pass, last_pass, ptrs, B, lane);
 }
 
-// The fill of pair p by one wave (all passes), its goal cell and, fused, its walk.
+// The fill of one n x m pair by one wave (all passes), its goal cell and,
+// when `walk`, its walk into `slot` (cigar_slot_bytes(n, m) bytes).  Q, T:
+// the sequences; ptrs: the pair's code workspace; B: its pass boundary row.
 template <int MODE, bool CIGAR, bool WIDE>
-__device__ __forceinline__ void fill_pair(const FillArgs& a, uint32_t p, int lane) {
-    const uint32_t n = a.qlen[p], m = a.tlen[p];
+__device__ __forceinline__ PairOut fill_one(const FillArgs& a, uint32_t n, uint32_t m, const uint8_t* Q,
+                                            const uint8_t* T, uint32_t* ptrs, int32_t* B, char* slot, bool walk,
+                                            int lane) {
+    const WalkSeq seq0{Q, T, 0, a.match, a.mismatch, a.gap};
     if (n == 0 || m == 0) {
-        if (lane == 0) degenerate<MODE>(a, p, n, m);
-        if (CIGAR && a.fused) {
+        PairOut o = degenerate<MODE>(a.gap, n, m);
+        if (CIGAR && walk) {
             // no cells: the walk is the closed-form boundary run (global/semi) or "1\0"
             const uint32_t gi = (MODE == kGlobal) ? n : 0, gj = (MODE == kGlobal || n == 0) ? m : 0;
-            fused_traceback<MODE>(a, p, nullptr, n, m, MODE == kLocal ? 0 : gi, MODE == kLocal ? 0 : gj, lane, 0);
+            traceback_pair<MODE>(nullptr, n, m, MODE == kLocal ? 0 : gi, MODE == kLocal ? 0 : gj, slot,
+                                 cigar_slot_bytes(n, m), lane, &o.cstart, &o.clen, seq0);
         }
-        return;
+        return o;
     }
-    const uint8_t* Q = a.qbytes + a.qoff[p];
-    const uint8_t* T = a.tbytes + a.toff[p];
     const uint32_t passes = n_passes(n);
-    uint32_t* ptrs = CIGAR ? a.ptrs + a.ptr_off[p] : nullptr;
-    int32_t* B = (passes > 1) ? a.bnd + a.bnd_off[p] : nullptr;
-
     // running goal over passes (wave-uniform); semi starts from (0,m), cost 0
     int best_h = (MODE == kSemi) ? 0 : INT_MIN;
     uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
@@ -366,20 +357,39 @@ __device__ __forceinline__ void fill_pair(const FillArgs& a, uint32_t p, int lan
         }
         if (MODE == kGlobal && last_pass) corner = o.corner;
         // the next pass reads this pass's bottom row (written by this wave)
-        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "agent");
+        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
     }
-    if (CIGAR && a.fused) {
+    PairOut o{(MODE == kGlobal) ? corner : best_h, (MODE == kLocal) ? best_j + 1 : 0u,  // :117-121 / :197-199 / :283-285
+              (MODE == kGlobal) ? n : best_i, (MODE == kGlobal) ? m : best_j, 0, 0};
+    if (CIGAR && walk) {
         // this wave's pointer stores -> its own loads in the walk
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        fused_traceback<MODE>(a, p, ptrs, n, m, (MODE == kGlobal) ? n : best_i, (MODE == kGlobal) ? m : best_j,
-                              lane, best_h);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        const WalkSeq seq{Q, T, best_h, a.match, a.mismatch, a.gap};
+        traceback_pair<MODE>(ptrs, n, m, o.gi, o.gj, slot, cigar_slot_bytes(n, m), lane, &o.cstart, &o.clen, seq);
     }
+    return o;
+}
+
+// fill_one for pair p of a plan chunk: per-pair arrays in, per-pair arrays out.
+template <int MODE, bool CIGAR, bool WIDE>
+__device__ __forceinline__ void fill_pair(const FillArgs& a, uint32_t p, int lane) {
+    const uint32_t n = a.qlen[p], m = a.tlen[p];
+    const bool walk = CIGAR && a.fused;
+    uint32_t* ptrs = (CIGAR && n && m) ? a.ptrs + a.ptr_off[p] : nullptr;
+    int32_t* B = (n_passes(n) > 1) ? a.bnd + a.bnd_off[p] : nullptr;
+    char* slot = walk ? a.slots + a.slot_off[p] : nullptr;
+    const PairOut o = fill_one<MODE, CIGAR, WIDE>(a, n, m, a.qbytes + a.qoff[p], a.tbytes + a.toff[p], ptrs, B, slot,
+                                                  walk, lane);
     if (lane == 0) {
-        a.score[p] = (MODE == kGlobal) ? corner : best_h;
-        a.target_begin[p] = (MODE == kLocal) ? best_j + 1 : 0;  // :117-121 / :197-199 / :283-285
-        a.goal_i[p] = (MODE == kGlobal) ? n : best_i;
-        a.goal_j[p] = (MODE == kGlobal) ? m : best_j;
+        a.score[p] = o.score;
+        a.target_begin[p] = o.tb;
+        a.goal_i[p] = o.gi;
+        a.goal_j[p] = o.gj;
+        if (walk) {
+            a.cigar_start[p] = a.slot_off[p] + o.cstart;
+            a.cigar_len[p] = o.clen;
+        }
     }
 }
 
@@ -393,59 +403,71 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
 
 #if TA_FILL_CIGAR
 // ---- the low-latency server (ta_internal.h ServeArgs; host side ta_server.cpp)
+// A relaxed system-scope load (bypasses the GPU caches; no cache invalidation):
+// the poll reads with it, and one acquire fence follows a detected request.
 __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // One request of slot s: copy the bytes into HBM, fill + walk, results back.
+// The request header and the first KB of each sequence come in one round trip
+// over PCIe (lanes 0-5 the header words, the others query bytes; a second load
+// per lane the target); longer sequences follow in a second round.
 template <int MODE>
-__device__ __forceinline__ void serve_one(const ServeArgs& sa, uint32_t s, char* slot, uint32_t seq, int lane) {
+__device__ __forceinline__ void serve_one(const ServeArgs& sa, uint32_t s, char* slot, uint32_t seq, int lane,
+                                          uint64_t t0) {
     ServeHdr* hd = reinterpret_cast<ServeHdr*>(slot);
     const uint32_t* req = reinterpret_cast<const uint32_t*>(slot);
-    // words 1..6: n, m, match, mismatch, gap, want_cigar (one round trip)
-    const uint32_t w = (lane < 6) ? sys_load(req + 1 + lane) : 0u;
+    const FillArgs& fa = sa.fa;
+    uint8_t* dq = const_cast<uint8_t*>(fa.qbytes) + (uint64_t)s * kSrvQMax;
+    uint8_t* dt = const_cast<uint8_t*>(fa.tbytes) + (uint64_t)s * kSrvTMax;
+    // lanes 0-5: words 1..6 (n, m, match, mismatch, gap, want_cigar); lanes 6-63: query bytes [0, 928)
+    uint4 qv = make_uint4(0, 0, 0, 0), tv;
+    uint32_t w = 0;
+    if (lane < 6) w = sys_load(req + 1 + lane);
+    else qv = *reinterpret_cast<const uint4*>(slot + kSrvQOff + 16u * (uint32_t)(lane - 6));
+    tv = *reinterpret_cast<const uint4*>(slot + kSrvTOff + 16u * (uint32_t)lane);  // target bytes [0, 1024)
     const uint32_t n = (uint32_t)rdlane((int)w, 0), m = (uint32_t)rdlane((int)w, 1);
-    const int ma = rdlane((int)w, 2), mi = rdlane((int)w, 3), gap = rdlane((int)w, 4);
+    FillArgs a = fa;
+    a.match = rdlane((int)w, 2);
+    a.mismatch = rdlane((int)w, 3);
+    a.gap = rdlane((int)w, 4);
     const bool want = rdlane((int)w, 5) != 0;
-    FillArgs a = sa.fa;
+    uint64_t t1 = t0, t2 = t0;  // phase clocks (100 MHz): request + bytes into HBM, fill + walk
     uint32_t status = TA_OK;
-    int score = 0;
-    uint32_t tb = 0, clen = 0;
+    PairOut o{0, 0, 0, 0, 0, 0};
+    char* cslot = a.slots + (uint64_t)s * ((cigar_slot_bytes(kSrvQMax, kSrvTMax) + 255) & ~255ull);
     if (n > kSrvQMax || m > kSrvTMax) {
         status = TA_ERR_ARG;  // (the host never posts such a pair)
     } else {
-        uint8_t* dq = const_cast<uint8_t*>(a.qbytes) + a.qoff[s];
-        uint8_t* dt = const_cast<uint8_t*>(a.tbytes) + a.toff[s];
-        for (uint32_t k = 16u * (uint32_t)lane; k < n; k += 1024u)
+        if (lane >= 6) *reinterpret_cast<uint4*>(dq + 16u * (uint32_t)(lane - 6)) = qv;
+        *reinterpret_cast<uint4*>(dt + 16u * (uint32_t)lane) = tv;
+        for (uint32_t k = 928u + 16u * (uint32_t)lane; k < n; k += 1024u)
             *reinterpret_cast<uint4*>(dq + k) = *reinterpret_cast<const uint4*>(slot + kSrvQOff + k);
-        for (uint32_t k = 16u * (uint32_t)lane; k < m; k += 1024u)
+        for (uint32_t k = 1024u + 16u * (uint32_t)lane; k < m; k += 1024u)
             *reinterpret_cast<uint4*>(dt + k) = *reinterpret_cast<const uint4*>(slot + kSrvTOff + k);
-        if (lane == 0) {
-            const_cast<uint32_t*>(a.qlen)[s] = n;
-            const_cast<uint32_t*>(a.tlen)[s] = m;
-        }
-        __threadfence();  // this wave's stores -> its own loads in the fill
-        a.match = ma;
-        a.mismatch = mi;
-        a.gap = gap;
-        a.fused = want ? 1 : 0;
-        fill_pair<MODE, true, false>(a, s, lane);
-        __threadfence();
-        score = a.score[s];
-        tb = a.target_begin[s];
-        if (want) {
-            clen = a.cigar_len[s];
-            const char* src = a.slots + a.cigar_start[s];
-            for (uint32_t k = (uint32_t)lane; k < clen; k += 64u) slot[kSrvCOff + k] = src[k];
-        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // this wave's stores -> its own loads
+        t1 = wall_clock64();
+        uint32_t* ptrs = fa.ptrs + (uint64_t)s * ptr_dwords(kSrvQMax, kSrvTMax);
+        int32_t* B = fa.bnd + (uint64_t)s * bnd_words(kSrvQMax, kSrvTMax);
+        o = fill_one<MODE, true, false>(a, n, m, dq, dt, ptrs, B, cslot, want, lane);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+        t2 = wall_clock64();
+        if (want)
+            for (uint32_t k = (uint32_t)lane; k < o.clen; k += 64u) slot[kSrvCOff + k] = cslot[o.cstart + k];
     }
+    const uint64_t t3 = wall_clock64();
     if (lane == 0) {
-        hd->score = score;
-        hd->target_begin = tb;
-        hd->cigar_len = clen;
+        hd->score = o.score;
+        hd->target_begin = o.tb;
+        hd->cigar_len = want ? o.clen : 0u;
         hd->status = status;
+        hd->pad1[0] = (uint32_t)(t1 - t0);  // diagnostics (ta_server_last_times), 10 ns units
+        hd->pad1[1] = (uint32_t)(t2 - t1);
+        hd->pad1[2] = (uint32_t)(t3 - t2);
     }
     __threadfence_system();  // results and CIGAR bytes visible to the host before `done`
+    if (lane == 0) hd->pad1[3] = (uint32_t)(wall_clock64() - t3);
     if (lane == 0) __hip_atomic_store(&hd->done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
@@ -469,7 +491,8 @@ __global__ __launch_bounds__(kWave) void serve_kernel(ServeArgs sa) {
         const uint32_t seq = (uint32_t)rdlane((int)v, 0), stop = (uint32_t)rdlane((int)v, 1),
                        hb = (uint32_t)rdlane((int)v, 2);
         if (seq != last) {
-            serve_one<MODE>(sa, s, slot, seq, lane);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request's bytes were written before seq
+            serve_one<MODE>(sa, s, slot, seq, lane, wall_clock64());
             last = seq;
             t_hb = wall_clock64();
             continue;

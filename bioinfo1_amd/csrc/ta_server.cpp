@@ -357,6 +357,13 @@ int ta_server_align(ta_server* s, const char* q, uint32_t n, const char* t, uint
     return rc;
 }
 
+int ta_server_last_times(const ta_server* s, uint32_t slot, double* us) {
+    if (!s || !us || slot >= s->slots) return TA_ERR_ARG;
+    const ta::ServeHdr* h = const_cast<ta_server*>(s)->hdr(slot);
+    for (int k = 0; k < 4; ++k) us[k] = h->pad1[k] * 0.01;  // 100 MHz ticks
+    return TA_OK;
+}
+
 int ta_server_running(const ta_server* s) {
     if (!s) return 0;
     std::lock_guard<std::mutex> lk(const_cast<ta_server*>(s)->mu);

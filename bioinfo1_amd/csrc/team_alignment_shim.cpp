@@ -241,9 +241,19 @@ int Align(const char* query, unsigned int query_len, const char* target, unsigne
     if (t != TA_GLOBAL && t != TA_LOCAL && t != TA_SEMI_GLOBAL)
         throw std::invalid_argument("Unknown AlignmentType provided.");  // team_alignment.cpp:73
     const int device = call_device();
-    if (server_enabled()) {
+    // A lone large pair (>= 256k cells, no other call on the server) finishes
+    // sooner as a one-pair batch (the packed kernel, both halves computing it)
+    // than on one int32 wave; concurrent calls are better off on the server.
+    static std::atomic<int> in_server{0};
+    const bool lone_large = (uint64_t)query_len * target_len >= (1u << 18) && in_server.load() == 0;
+    if (server_enabled() && !lone_large) {
         ta_server* srv = server_for(device, t);
         if (srv && ta_server_fits(srv, query_len, target_len, match, mismatch, gap)) {
+            struct Count {
+                std::atomic<int>& c;
+                explicit Count(std::atomic<int>& x) : c(x) { c.fetch_add(1); }
+                ~Count() { c.fetch_sub(1); }
+            } count(in_server);
             thread_local std::vector<char> cbuf;
             const uint64_t cap = ta_cigar_slot_bytes(query_len, target_len);
             if (cigar && cbuf.size() < cap) cbuf.resize(cap);

@@ -89,6 +89,10 @@ int ta_server_align(ta_server* server, const char* query, uint32_t query_len, co
                     uint32_t* target_begin, char* cigar, uint64_t cigar_capacity, uint32_t* cigar_len);
 /* 1 while the server's kernel is resident. */
 int ta_server_running(const ta_server* server);
+/* Diagnostics: the device-side phase times (microseconds) of the last request
+ * served in `slot`: [0] request + bytes into HBM, [1] fill + walk, [2] results
+ * and CIGAR into the slot, [3] the system-scope release fence. */
+int ta_server_last_times(const ta_server* server, uint32_t slot, double* us_out4);
 
 /* The drop-in team::Align (include/team_alignment.hpp) runs each call on:
  * the device set here (device >= 0; -1 clears the choice), else the device

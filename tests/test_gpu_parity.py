@@ -695,3 +695,25 @@ def test_single_pair_server(kat_cases, random_cases, oracle):
 
 def want_score_cfg1(mode):
     return {0: -1, 1: 3, 2: 2}[mode]  # SURVEY §4 table 2, GTACC / GATACGTTA
+
+
+def test_host_pipeline(aligner, oracle):
+    """align.HostPipeline (host inputs -> host results, transfers overlapped with
+    the kernels, two plans alternating): after several steps the last results
+    equal the oracle's, in all modes and score-only."""
+    from bioinfo1_amd.align import HostPipeline
+
+    b = synth.related_batch(300, 700, 650, seed=41)
+    for mode in (0, 1, 2):
+        want = oracle.align_batch(b, mode, 1, -1, -1, True)
+        for cig in (True, False):
+            hp = HostPipeline(aligner, b, mode, 1, -1, -1, cig)
+            for _ in range(5):
+                hp.step()
+            hp.drain()
+            r = hp.results()
+            hp.close()
+            np.testing.assert_array_equal(r.scores, want.scores)
+            np.testing.assert_array_equal(r.target_begins, want.target_begins)
+            if cig:
+                assert r.cigars() == want.cigars()
