@@ -91,3 +91,43 @@ def test_mapper_cli_help_and_version():
     assert r.returncode == 0 and "-a, --alignment TYPE" in r.stdout
     r = M.run_cli([], text=True)
     assert r.returncode == 1 and "Not enough arguments" in r.stderr
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isfile(os.path.join(REF, "team_alignment", "team_alignment.hpp")),
+                    reason="reference sources absent (GPU box)")
+def test_reference_header_and_minimizers_link_against_library():
+    """The reference's own team_alignment.hpp (read in place, not copied) and its
+    team_minimizers.cpp, with a caller shaped like team_mapper.cpp:666-678 (cigar or
+    nullptr, &ref_offset, inside try/catch), link into an executable against
+    libteam_alignment.so alone: team::Align resolves from our library and the link
+    leaves nothing undefined.  team_mapper.cpp itself includes bioparser
+    (team_mapper.cpp:13-14), an un-vendored submodule absent here; a stand-in for
+    it would be a reference build from stand-ins, so that file is not compiled."""
+    src = ('#include <string>\n#include <stdexcept>\n#include <cstdio>\n'
+           '#include "team_alignment.hpp"\n#include "team_minimizers.hpp"\nusing namespace team;\n'
+           'int main(int argc, char**){ std::string cigar; unsigned ref_offset = 0; int score = 0;\n'
+           '  KMER frag(true); auto mins = frag.Minimize("ACGTACGTAC", 10, 3, 2); (void)mins;\n'
+           '  try { score = team::Align("ACGT", 4, "AACGTT", 6, team::AlignmentType::local, 1, -1, -1,\n'
+           '                            argc > 1 ? &cigar : nullptr, &ref_offset); }\n'
+           '  catch (const std::exception& e) { std::fprintf(stderr, "%s\\n", e.what()); return 1; }\n'
+           '  return score; }\n')
+    tmp = os.path.join(ROOT, "build", "ref_link_probe")
+    os.makedirs(tmp, exist_ok=True)
+    with open(os.path.join(tmp, "caller.cpp"), "w") as f:
+        f.write(src)
+    exe = os.path.join(tmp, "caller")
+    libdir = os.path.dirname(A.LIB_PATH)
+    subprocess.check_call(["g++", "-std=c++17", "-O1",
+                           "-I", os.path.join(REF, "team_alignment"), "-I", os.path.join(REF, "team_minimizers"),
+                           os.path.join(tmp, "caller.cpp"), os.path.join(REF, "team_minimizers", "team_minimizers.cpp"),
+                           "-L", libdir, "-lteam_alignment", "-Wl,-rpath," + libdir, "-Wl,--no-undefined",
+                           "-o", exe])
+    und = subprocess.check_output(["nm", "-u", exe], text=True)
+    assert A.TEAM_ALIGN_SYMBOL in und           # not defined in the executable ...
+    dyn = subprocess.check_output(["readelf", "-d", exe], text=True)
+    assert "libteam_alignment.so" in dyn        # ... but bound to our library
+    defined = subprocess.check_output(["nm", "-D", "--defined-only", A.LIB_PATH], text=True)
+    assert A.TEAM_ALIGN_SYMBOL in defined
