@@ -119,6 +119,7 @@ def lib() -> C.CDLL:
     L.ta_affine_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
     L.ta_affine_plan_execute_fill.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
     L.ta_affine_plan_execute_traceback.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32]
+    L.ta_affine_plan_check.argtypes = [C.c_void_p]
     # the low-latency single-pair server (ta_server_*)
     L.ta_server_create.argtypes = [C.c_int, C.c_int, C.c_uint32, C.POINTER(C.c_void_p)]
     L.ta_server_destroy.argtypes = [C.c_void_p]
@@ -142,7 +143,7 @@ ABI_SYMBOLS = [
     "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_pair_chunks", "ta_affine_plan_pair_chunks", "ta_plan_execute_traceback", "ta_compact_cigars",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
-    "ta_affine_plan_execute_traceback", "ta_align_batch_affine",
+    "ta_affine_plan_execute_traceback", "ta_affine_plan_check", "ta_align_batch_affine",
     "ta_server_create", "ta_server_destroy", "ta_server_fits", "ta_server_align", "ta_server_running",
     "ta_server_last_times",
 ]
@@ -448,10 +449,9 @@ class DevicePlan:
     def check(self):
         """ta_plan_check after synchronising: raises DeviceError if a kernel reported an internal failure."""
         self.torch.cuda.synchronize(self.dev)
-        if not self.affine:
-            r = lib().ta_plan_check(self._h)
-            if r != TA_OK:
-                _raise(r, self._ctx)
+        r = self._fn("ta_plan_check")(self._h)
+        if r != TA_OK:
+            _raise(r, self._ctx)
 
     def compact_cigars(self):
         """The CIGARs packed back to back on the device (ta_compact_cigars on

@@ -75,6 +75,14 @@ struct AffArgs {
     const uint32_t* count_dev;  // non-null: wave count read on the device (the dual fill's hand-back list)
     uint32_t* fb_list;          // dual fill: couples handed back to the int32 fill ('-' in a query)
     uint32_t* fb_count;
+    // dual fill, one wave per (couple, pass): ticket t is pass
+    // t / count of couple t % count (pass-major), n_tasks = count * the chunk's
+    // largest pass count; passes hand their bottom row over tagged records
+    uint32_t* ticket;  // zeroed before the launch
+    uint32_t n_tasks;
+    uint32_t epoch;    // tag base of this launch's records
+    uint32_t* err;     // a poll gave up (never on a correct schedule)
+    void* pout;        // PassOut[2] per (pass, couple): [(pass * count + w) * 2 + h]
 };
 
 // 64 boundary entries per chunk: column 64k+lane+1.
@@ -470,6 +478,46 @@ __global__ __launch_bounds__(kBlock) void affine_traceback_kernel(AffArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Pass hand-off of the packed affine fill.  Each pass of a couple runs on its
+// own wave; pass p's bottom row goes to 8-byte records tag << 32 | packed
+// value ([2j] = H of both pairs, [2j + 1] = F), written with relaxed
+// agent-scope (sc1) stores by the lane holding row 1024(p+1); pass p+1 polls
+// a 64-column chunk with sc1 loads until every record carries the tag it
+// expects (the data is its own flag, as the flexible fill's, ta_flex.hip).
+// Two buffers alternate by pass parity.
+typedef __attribute__((address_space(1))) unsigned long long gu64a;
+
+struct AffRec {
+    uint64_t* w;        // this pass's bottom row (null on the last pass)
+    const uint64_t* r;  // the previous pass's (null on pass 0)
+    uint32_t tag_w, tag_r;
+    uint32_t* err;
+};
+
+// columns 64k + lane + 1 of the previous pass's bottom row: (H, F) packed
+__device__ __forceinline__ uint2 aff_poll_chunk(const AffRec& rc, uint32_t m, uint32_t k, int lane) {
+    const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+    const gu64a* r = (const gu64a*)(rc.r + 2ull * j);
+    uint2 v = make_uint2(0, 0);
+    for (uint32_t spins = 0;; ++spins) {
+        bool ok = true;
+        if (j <= m) {
+            const uint64_t x = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t y = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(x >> 32) == rc.tag_r && (uint32_t)(y >> 32) == rc.tag_r;
+            v = make_uint2((uint32_t)x, (uint32_t)y);
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spins > (1u << 22)) {  // bounded: the kernel always ends
+            if (lane == 0) atomicOr(rc.err, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return v;
+}
+
+// ---------------------------------------------------------------------------
 // Packed two-pair affine fill (global / semi-global): two pairs of the same
 // (n, m) per wave, pair A in bits 15:0 and pair B in bits 31:16 of every
 // register, v_pk_* arithmetic.  Same geometry and the same 4-bit codes as
@@ -489,8 +537,8 @@ __global__ __launch_bounds__(kBlock) void affine_traceback_kernel(AffArgs a) {
 // (ta_packed.h mismatch_table / row_selector), one v_perm per row.
 template <int MODE, bool CIGAR, int NV, bool CLS>
 __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* const (&Q)[2], const uint8_t* const (&T)[2],
-                                              uint2* const (&ptrs)[2], uint2* B, uint32_t n, uint32_t m, uint32_t pass,
-                                              bool last_pass, bool tdash, int lane, PassOut (&out)[2]) {
+                                              uint2* const (&ptrs)[2], const AffRec& rc, uint32_t n, uint32_t m,
+                                              uint32_t pass, bool last_pass, bool tdash, int lane, PassOut (&out)[2]) {
     constexpr int R = kRows;
     const int ma = a.match, mi = a.mismatch, O = a.open, X = a.extend;
     const int OX = O + X;
@@ -531,15 +579,10 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
         tcur[h] = load_tchunk(T[h], m, 0, lane);
         tnext[h] = load_tchunk(T[h], m, 1, lane);
     }
-    uint2 bcur = make_uint2(0, 0), bnext = make_uint2(0, 0);
-    auto load_b = [&](uint32_t k) {
-        const uint32_t j = k * 64u + (uint32_t)lane + 1u;
-        return j <= m ? B[j] : make_uint2(0, 0);
-    };
-    if (pass > 0) {
-        bcur = load_b(0);
-        bnext = load_b(1);
-    }
+    // the previous pass's bottom row, polled one 64-column chunk at a time just
+    // before it is needed
+    uint2 bcur = make_uint2(0, 0);
+    if (pass > 0) bcur = aff_poll_chunk(rc, m, 0, lane);
     const uint32_t steps = m + nl - 1;
     uint2* prow0 = CIGAR ? ptrs[0] + (uint64_t)pass * Tmax * kWave : nullptr;
     uint2* prow1 = CIGAR ? ptrs[1] + (uint64_t)pass * Tmax * kWave : nullptr;
@@ -552,10 +595,7 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
                 tnext[h] = load_tchunk(T[h], m, (t >> 8) + 1, lane);
             }
         }
-        if (pass > 0) {
-            bcur = bnext;
-            bnext = load_b((t >> 6) + 1);
-        }
+        if (pass > 0) bcur = aff_poll_chunk(rc, m, t >> 6, lane);
     };
     auto step = [&](uint32_t t, auto masked_tag) {
         constexpr bool MASKED = decltype(masked_tag)::value;
@@ -634,7 +674,12 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
                 rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jj, rowbest_j);
                 rowbest = pk_max(rowbest, v);
             }
-            if (has_next && (uint32_t)lane == nl - 1) B[j] = make_uint2(H2[R - 1], Flast);
+            if (has_next && (uint32_t)lane == nl - 1) {
+                const uint64_t tg = (uint64_t)rc.tag_w << 32;
+                gu64a* wr = (gu64a*)(rc.w + 2ull * j);
+                __hip_atomic_store(wr, tg | H2[R - 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(wr + 1, tg | Flast, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         }
         if (CIGAR) {
             // 32-bit byte offset from the uniform row base (SGPR base + VGPR offset stores)
@@ -698,15 +743,15 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
 
 template <int MODE, bool CIGAR, bool CLS>
 __device__ __forceinline__ void aff_dual_pass_nv(const AffArgs& a, const uint8_t* const (&Q)[2],
-                                                 const uint8_t* const (&T)[2], uint2* const (&ptrs)[2], uint2* B,
-                                                 uint32_t n, uint32_t m, uint32_t pass, bool last_pass, bool tdash,
-                                                 int lane, PassOut (&out)[2]) {
+                                                 const uint8_t* const (&T)[2], uint2* const (&ptrs)[2],
+                                                 const AffRec& rc, uint32_t n, uint32_t m, uint32_t pass,
+                                                 bool last_pass, bool tdash, int lane, PassOut (&out)[2]) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
     if (MODE == kGlobal || nv == kRows || !last_pass)
-        return aff_dual_pass<MODE, CIGAR, kRows, CLS>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
+        return aff_dual_pass<MODE, CIGAR, kRows, CLS>(a, Q, T, ptrs, rc, n, m, pass, last_pass, tdash, lane, out);
 #define TA_NV_CASE(k) \
-    case k: return aff_dual_pass<MODE, CIGAR, k, CLS>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, out);
+    case k: return aff_dual_pass<MODE, CIGAR, k, CLS>(a, Q, T, ptrs, rc, n, m, pass, last_pass, tdash, lane, out);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -715,16 +760,30 @@ __device__ __forceinline__ void aff_dual_pass_nv(const AffArgs& a, const uint8_t
 #undef TA_NV_CASE
 }
 
-// order: 2 pair ids per wave (same n and m, values within int16)
+constexpr uint32_t kAffSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to the int32 fill
+
+// order: 2 pair ids per couple (same n and m, values within int16).  One wave
+// per (couple, pass): a wave takes the next ticket, pass-major (every couple's
+// pass 0, then every pass 1, ...), so the pass it polls belongs to a wave that
+// took an earlier ticket and is running -- every poll ends -- and a chunk of
+// long couples (config 5: 2,048 couples x 10 passes) fills every wave slot
+// instead of two per SIMD.  Each wave writes its pass's PassOut; a combine
+// kernel folds them.
 template <int MODE, bool CIGAR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void affine_dual_fill_kernel(AffArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint32_t widx = wave_id();
-    if (widx >= a.count) return;
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(a.ticket, 1u);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+    if (tk >= a.n_tasks) return;
+    const uint32_t pass = tk / a.count, w = tk - pass * a.count;
     uint32_t p[2];
-    p[0] = a.order[2 * (a.begin + widx)];
-    p[1] = a.order[2 * (a.begin + widx) + 1];
+    p[0] = a.order[2 * (a.begin + w)];
+    p[1] = a.order[2 * (a.begin + w) + 1];
     const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
+    const uint32_t passes = n_passes(n);
+    if (pass >= passes) return;
+    PassOut* po = static_cast<PassOut*>(a.pout) + 2ull * ((uint64_t)pass * a.count + w);
     const uint8_t* Q[2];
     const uint8_t* T[2];
     uint2* ptrs[2];
@@ -742,57 +801,75 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
         }
     }
     const bool cls = __ballot(qother) == 0;
-    if (__ballot(qdash)) {  // per-row vertical gap constants: the int32 fill takes the couple
+    if (__ballot(qdash)) {  // per-row vertical gap constants: the int32 fill takes the couple (pass 0 hands it over)
         if (lane == 0) {
-            // a self-coupled pair (p[0] == p[1], ta_planner.cpp) is handed back once:
-            // two int32 waves on one pair would share its in-place boundary row
-            const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
-            const uint32_t at = atomicAdd(a.fb_count, k);
-            a.fb_list[at] = p[0];
-            if (k == 2) a.fb_list[at + 1] = p[1];
+            if (pass == 0) {
+                // a self-coupled pair (p[0] == p[1]) is handed back once
+                const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
+                const uint32_t at = atomicAdd(a.fb_count, k);
+                a.fb_list[at] = p[0];
+                if (k == 2) a.fb_list[at + 1] = p[1];
+            }
+            po[0].i = kAffSkip;
+            po[1].i = kAffSkip;
         }
         return;
     }
     tdash = __ballot(tdash) != 0;
-    const uint32_t passes = n_passes(n);
-    uint2* B = (passes > 1) ? reinterpret_cast<uint2*>(a.bnd + a.bnd_off[p[0]]) : nullptr;
-    int best_h[2], corner[2] = {0, 0};
-    uint32_t best_i[2], best_j[2];
+    const bool last_pass = pass + 1 == passes;
+    AffRec rc;
+    uint64_t* rec = reinterpret_cast<uint64_t*>(a.bnd + a.bnd_off[p[0]]);  // 2 buffers x 2(m+1) records
+    const uint64_t rb = 2ull * (m + 1);
+    rc.w = last_pass ? nullptr : rec + (pass & 1u) * rb;
+    rc.r = pass ? rec + ((pass - 1u) & 1u) * rb : nullptr;
+    // never 0, unique per launch and pass (passes < 64: affine_fits_int16); the
+    // host zeroes the records before each launch
+    rc.tag_w = a.epoch * 64u + pass + 1u;
+    rc.tag_r = a.epoch * 64u + pass;
+    rc.err = a.err;
+    PassOut o[2];
+    if (cls) aff_dual_pass_nv<MODE, CIGAR, true>(a, Q, T, ptrs, rc, n, m, pass, last_pass, tdash, lane, o);
+    else aff_dual_pass_nv<MODE, CIGAR, false>(a, Q, T, ptrs, rc, n, m, pass, last_pass, tdash, lane, o);
+    if (lane == 0) {
+        po[0] = o[0];
+        po[1] = o[1];
+    }
+}
+
+// After the packed fill: fold each couple's per-pass results in pass order
+// (semi: the upper pass wins ties on column m, then row n strictly above,
+// :265-278; global: the last pass's corner).
+template <int MODE>
+__global__ void affine_dual_combine_kernel(AffArgs a) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= a.count) return;
+    const PassOut* po = static_cast<const PassOut*>(a.pout);
+    if (po[2ull * w].i == kAffSkip) return;
+    const uint32_t p0 = a.order[2 * (a.begin + w)];
+    const uint32_t n = a.qlen[p0], m = a.tlen[p0], passes = n_passes(n);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        best_h[h] = (MODE == kSemi) ? 0 : INT_MIN;  // semi starts from (0,m), cost 0
-        best_i[h] = 0;
-        best_j[h] = (MODE == kSemi) ? m : 0;
-    }
-    for (uint32_t pass = 0; pass < passes; ++pass) {
-        const bool last_pass = pass + 1 == passes;
-        PassOut o[2];
-        if (cls) aff_dual_pass_nv<MODE, CIGAR, true>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, o);
-        else aff_dual_pass_nv<MODE, CIGAR, false>(a, Q, T, ptrs, B, n, m, pass, last_pass, tdash, lane, o);
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            if (MODE == kSemi && o[h].h > best_h[h]) {  // strict: the upper pass wins ties
-                best_h[h] = o[h].h;
-                best_i[h] = o[h].i;
-                best_j[h] = o[h].j;
+        const uint32_t p = a.order[2 * (a.begin + w) + h];
+        int best_h = (MODE == kSemi) ? 0 : INT_MIN, corner = 0;  // semi starts from (0,m), cost 0
+        uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
+        for (uint32_t k = 0; k < passes; ++k) {
+            const PassOut& o = po[2ull * ((uint64_t)k * a.count + w) + h];
+            if (MODE == kSemi && o.h > best_h) {
+                best_h = o.h;
+                best_i = o.i;
+                best_j = o.j;
             }
-            if (MODE == kSemi && last_pass && o[h].row_h > best_h[h]) {  // row n after column m (:271-278)
-                best_h[h] = o[h].row_h;
-                best_i[h] = n;
-                best_j[h] = o[h].row_j;
+            if (MODE == kSemi && k + 1 == passes && o.row_h > best_h) {
+                best_h = o.row_h;
+                best_i = n;
+                best_j = o.row_j;
             }
-            if (MODE == kGlobal && last_pass) corner[h] = o[h].corner;
+            if (MODE == kGlobal && k + 1 == passes) corner = o.corner;
         }
-        if (!last_pass) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // boundary row -> next pass
-    }
-    if (lane == 0) {
-#pragma unroll
-        for (int h = 0; h < 2; ++h) {
-            a.score[p[h]] = (MODE == kGlobal) ? corner[h] : best_h[h];
-            a.target_begin[p[h]] = 0;
-            a.goal_i[p[h]] = (MODE == kGlobal) ? n : best_i[h];
-            a.goal_j[p[h]] = (MODE == kGlobal) ? m : best_j[h];
-        }
+        a.score[p] = (MODE == kGlobal) ? corner : best_h;
+        a.target_begin[p] = 0;
+        a.goal_i[p] = (MODE == kGlobal) ? n : best_i;
+        a.goal_j[p] = (MODE == kGlobal) ? m : best_j;
     }
 }
 
@@ -800,7 +877,7 @@ inline dim3 aff_grid(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) 
 
 hipError_t launch_affine_dual(int mode, bool cigar, const AffArgs& a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
-    const dim3 g = aff_grid(a.count), b(kBlock);
+    const dim3 g = aff_grid(a.n_tasks), b(kBlock), gc((a.count + 255) / 256), bc(256);
     switch (mode * 2 + (cigar ? 1 : 0)) {
         case kGlobal * 2: hipLaunchKernelGGL((affine_dual_fill_kernel<kGlobal, false>), g, b, 0, s, a); break;
         case kGlobal * 2 + 1: hipLaunchKernelGGL((affine_dual_fill_kernel<kGlobal, true>), g, b, 0, s, a); break;
@@ -808,6 +885,8 @@ hipError_t launch_affine_dual(int mode, bool cigar, const AffArgs& a, hipStream_
         case kSemi * 2 + 1: hipLaunchKernelGGL((affine_dual_fill_kernel<kSemi, true>), g, b, 0, s, a); break;
         default: return hipErrorInvalidValue;
     }
+    if (mode == kGlobal) hipLaunchKernelGGL(affine_dual_combine_kernel<kGlobal>, gc, bc, 0, s, a);
+    else hipLaunchKernelGGL(affine_dual_combine_kernel<kSemi>, gc, bc, 0, s, a);
     return hipGetLastError();
 }
 
@@ -854,6 +933,8 @@ struct ta_affine_plan {
     uint32_t *d_singles = nullptr, *d_duals = nullptr;
     uint32_t* d_fb = nullptr;  // hand-back list [2 * couples], then one counter per chunk
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
+    uint32_t *d_err = nullptr, *d_tickets = nullptr;  // packed fill: poll error word, one ticket counter per chunk
+    void* d_pout = nullptr;                           // PassOut[2] per (pass, couple) of one chunk
 };
 
 namespace {
@@ -861,9 +942,16 @@ namespace {
 using ta_host::fail;
 
 struct AffOffs {
-    uint64_t qlen, tlen, order, singles, duals, ptr_off, bnd_off, slot_off;  // uploaded
-    uint64_t goal_i, goal_j, fb;                                             // device-only
+    uint64_t qlen, tlen, order, singles, duals, ptr_off, bnd_off, slot_off, err, tickets;  // uploaded
+    uint64_t goal_i, goal_j, fb, pout;                                                    // device-only
 };
+
+// PassOut[2] per (pass, couple) of the largest chunk (24-byte PassOut)
+uint64_t aff_pout_bytes(const ta::AffinePlan& h) {
+    uint64_t n = 0;
+    for (const auto& ch : h.chunks) n = std::max<uint64_t>(n, 2ull * ch.dcount * ch.dpasses);
+    return n * 24ull;
+}
 
 template <class T>
 uint64_t avbytes(const std::vector<T>& v) {
@@ -880,6 +968,8 @@ AffOffs aff_layout(const ta::AffinePlan& h, ta::BlockLayout& L) {
     o.ptr_off = L.add(avbytes(h.ptr_off));
     o.bnd_off = L.add(avbytes(h.bnd_off));
     o.slot_off = L.add(avbytes(h.slot_off));
+    o.err = L.add(4);
+    o.tickets = L.add(4ull * h.chunks.size());
     return o;
 }
 
@@ -887,6 +977,7 @@ void aff_layout_scratch(const ta::AffinePlan& h, ta::BlockLayout& L, AffOffs& o)
     o.goal_i = L.add(4ull * h.n_pairs);
     o.goal_j = L.add(4ull * h.n_pairs);
     o.fb = L.add(4ull * (h.duals.size() + h.chunks.size()));
+    o.pout = L.add(aff_pout_bytes(h));
 }
 
 void aff_pack(const ta::AffinePlan& h, const AffOffs& o, uint8_t* base) {
@@ -901,6 +992,8 @@ void aff_pack(const ta::AffinePlan& h, const AffOffs& o, uint8_t* base) {
     put(o.ptr_off, h.ptr_off);
     put(o.bnd_off, h.bnd_off);
     put(o.slot_off, h.slot_off);
+    std::memset(base + o.err, 0, 4);
+    std::memset(base + o.tickets, 0, 4ull * h.chunks.size());
 }
 
 void aff_bind(ta_affine_plan* pl, uint8_t* d, const AffOffs& o) {
@@ -917,6 +1010,9 @@ void aff_bind(ta_affine_plan* pl, uint8_t* d, const AffOffs& o) {
     pl->d_goal_i = u32(o.goal_i);
     pl->d_goal_j = u32(o.goal_j);
     pl->d_fb = u32(o.fb);
+    pl->d_err = u32(o.err);
+    pl->d_tickets = u32(o.tickets);
+    pl->d_pout = d + o.pout;
 }
 
 // the oracle's range (oracle_affine_in_range): every |value| < 2^26
@@ -996,6 +1092,15 @@ int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s,
             d.count = ch.dcount;
             d.fb_list = fb_list;
             d.fb_count = fb_count;
+            // one wave per (couple, pass), tickets pass-major; the hand-off records
+            // start zeroed (tags are small integers; the region may hold old codes)
+            d.ticket = pl->d_tickets + c;
+            d.n_tasks = ch.dcount * ch.dpasses;
+            d.epoch = ++ctx->epoch & 0x3FFFFFFu;
+            d.err = pl->d_err;
+            d.pout = pl->d_pout;
+            TA_HIP(ctx, hipMemsetAsync(d.ticket, 0, 4, s));
+            if (ch.dpasses > 1) TA_HIP(ctx, hipMemsetAsync(ctx->ws_bnd.p, 0, ch.bnd_entries * sizeof(int2), s));
             TA_HIP(ctx, ta::launch_affine_dual(h.type, h.want_cigar, d, s));
             ta::AffArgs f = a;
             f.order = fb_list;
@@ -1042,8 +1147,10 @@ struct AffineHostPlan final : ta_host::HostPlan {
         return affine_exec(pl, io, s, UINT32_MAX, true, true);
     }
     uint64_t slots_bytes() const override { return pl->h.slots_bytes; }
-    uint64_t err_offset() const override { return UINT64_MAX; }
-    const char* err_message() const override { return ""; }
+    uint64_t err_offset() const override { return pl->h.duals.empty() ? UINT64_MAX : o.err; }
+    const char* err_message() const override {
+        return "packed affine fill: a pass hand-off poll timed out; results of this batch are invalid";
+    }
 };
 
 }  // namespace
@@ -1088,6 +1195,18 @@ int ta_affine_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qle
 }
 
 uint64_t ta_affine_plan_cigar_slots_bytes(const ta_affine_plan* pl) { return pl ? pl->h.slots_bytes : 0; }
+
+int ta_affine_plan_check(ta_affine_plan* pl) {
+    if (!pl) return TA_ERR_ARG;
+    if (pl->h.duals.empty()) return TA_OK;
+    uint32_t err = 0;
+    TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
+    TA_HIP(pl->ctx, hipMemcpy(&err, pl->d_err, 4, hipMemcpyDeviceToHost));
+    if (!err) return TA_OK;
+    TA_HIP(pl->ctx, hipMemset(pl->d_err, 0, 4));
+    return fail(pl->ctx, TA_ERR_DEVICE,
+                "packed affine fill: a pass hand-off poll timed out; results of this plan are invalid");
+}
 uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* pl) {
     return pl ? pl->h.ws_ptr_entries * sizeof(uint2) + pl->h.ws_bnd_entries * sizeof(int2) : 0;
 }

@@ -369,15 +369,19 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
     const uint64_t budget_entries = std::max<uint64_t>(budget / 8, 1);
     pl.ptr_off.assign(n_pairs, 0);
     pl.bnd_off.assign(n_pairs, 0);
-    AffinePlan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0};
+    AffinePlan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0, 0};
     auto unit_codes = [&](size_t k) -> uint64_t {
         const auto& u = units[k];
         if (!want_cigar) return 0;
         return ptr_dwords(qlen[u.first], tlen[u.first]) +
                (u.second == UINT32_MAX ? 0 : ptr_dwords(qlen[u.second], tlen[u.second]));
     };
-    const std::vector<size_t> starts =
-        chunk_starts(units.size(), budget_entries, wave_quantum, unit_codes, [](size_t) -> uint64_t { return 1; });
+    // the packed fill runs one wave per (couple, pass); the int32 fill one per pair
+    auto unit_waves = [&](size_t k) -> uint64_t {
+        const auto& u = units[k];
+        return u.second == UINT32_MAX ? 1 : n_passes(qlen[u.first]);
+    };
+    const std::vector<size_t> starts = chunk_starts(units.size(), budget_entries, wave_quantum, unit_codes, unit_waves);
     size_t next_cut = 1;
     for (size_t k = 0; k < units.size(); ++k) {
         const auto& u = units[k];
@@ -385,7 +389,7 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
         const int cnt = u.second == UINT32_MAX ? 1 : 2;
         if (next_cut < starts.size() && k == starts[next_cut]) {
             pl.chunks.push_back(c);
-            c = {(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0, (uint32_t)(pl.duals.size() / 2), 0, 0, 0};
+            c = {(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0, (uint32_t)(pl.duals.size() / 2), 0, 0, 0, 0};
             ++next_cut;
         }
         for (int h = 0; h < cnt; ++h) {
@@ -393,7 +397,12 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
             pl.ptr_off[p] = c.ptr_entries;
             pl.bnd_off[p] = c.bnd_entries;
             c.ptr_entries += want_cigar ? ptr_dwords(qlen[p], tlen[p]) : 0;
-            c.bnd_entries += bnd_words(qlen[p], tlen[p]);
+            // a multi-pass couple's pair A holds the pass hand-off records: 2 buffers x
+            // (H, F) x 8 bytes per column = 4 int2 entries; pair B keeps its own
+            // boundary row for the int32 fallback ('-' in a query)
+            uint64_t bw = bnd_words(qlen[p], tlen[p]);
+            if (cnt == 2 && h == 0 && n_passes(qlen[p]) > 1) bw = std::max<uint64_t>(bw, 4ull * ((uint64_t)tlen[p] + 1));
+            c.bnd_entries += bw;
             pl.order.push_back(p);
             ++c.count;
         }
@@ -401,6 +410,7 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
             pl.duals.push_back(u.first);
             pl.duals.push_back(u.second);
             ++c.dcount;
+            c.dpasses = std::max(c.dpasses, n_passes(qlen[u.first]));
         } else {
             pl.singles.push_back(u.first);
             ++c.scount;

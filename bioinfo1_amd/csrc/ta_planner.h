@@ -83,6 +83,7 @@ struct AffinePlan {
         uint32_t sbegin, scount;  // singles
         uint32_t dbegin, dcount;  // couples
         uint64_t ptr_entries, bnd_entries;
+        uint32_t dpasses;         // largest pass count of the chunk's couples (one wave per couple and pass)
     };
     std::vector<Chunk> chunks;
     uint64_t slots_bytes = 0, ws_ptr_entries = 0, ws_bnd_entries = 0;

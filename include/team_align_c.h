@@ -255,6 +255,9 @@ int ta_affine_plan_execute(ta_affine_plan* plan, const ta_device_io* io, void* h
 int ta_affine_plan_execute_fill(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream, uint32_t chunk);
 int ta_affine_plan_execute_traceback(ta_affine_plan* plan, const ta_device_io* io, void* hip_stream,
                                      uint32_t chunk);
+/* As ta_plan_check: TA_ERR_DEVICE when a pass hand-off poll of the packed
+ * affine fill (one wave per couple and pass) gave up; clears the flag. */
+int ta_affine_plan_check(ta_affine_plan* plan);
 
 /* Host-memory batch with affine gaps: ta_align_batch with gap -> (gap_open, gap_extend). */
 int ta_align_batch_affine(ta_context* ctx, uint32_t n_pairs, const char* query_bytes, const uint64_t* query_off,
