@@ -409,13 +409,206 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---- small pairs (n <= 64, m <= 1024): one query row per lane, all in LDS.
+// The batch fill gives a lane 16 rows; for one lone pair that makes every step
+// a 16-row dependent chain on an otherwise idle CU (a 5x9 pair: ~11 us of fill
+// and walk, 200x200 ~170 us).  Here lane l owns row l + 1 and steps along the
+// anti-diagonals (lane l at column t - l + 1 at step t; up and diag arrive
+// from lane l - 1 by DPP wave_shr:1 as in the batch fill), with the
+// reference's int32 cell rule verbatim (team_alignment.cpp:102-116 / :172-194 /
+// :250-263: strict '>' in the order MATCH, INSERT, DELETE; '-' free gaps; the
+// local clamp and first strict row-major maximum; the semi-global column-m
+// then row-n goal).  Codes: 2 bits per cell (M 0, I 1, D 2, local cost 0 =
+// STOP 3), 16 steps per dword, [step / 16][lane] in LDS.  The walk (:123-138,
+// :201-217, :286-315) runs on uniform values reading LDS, the RLE is formatted
+// lane-parallel (:145-160, "1\0" for an empty op string) and goes straight
+// into the host slot.
+constexpr uint32_t kSmallQ = 64, kSmallT = 1024;
+constexpr uint32_t kSmallCodeDw = (kSmallT + kSmallQ - 1 + 15) / 16 * kWave;
+struct SmallLds {
+    uint32_t codes[kSmallCodeDw];
+    uint32_t runs[kSmallQ + kSmallT + 4];
+    uint8_t q[kSmallQ];
+    uint8_t t[kSmallT];
+    char text[2 * (kSmallQ + kSmallT) + 16];
+};
+
+template <int MODE>
+__device__ __forceinline__ PairOut serve_small(const FillArgs& a, uint32_t n, uint32_t m, bool want, SmallLds& L,
+                                               char* out_text, int lane) {
+    const int ma = a.match, mi = a.mismatch, gap = a.gap;
+    const int init = (MODE == kGlobal) ? gap : 0;  // :62-74
+    const uint32_t l = (uint32_t)lane;
+    const bool row = l < n;
+    const uint32_t qb = L.q[min(l, n - 1u)];
+    const int upg = (qb == (uint32_t)'-') ? 0 : gap;  // indel(query[i-1]), :25-28
+    int H = wmul(l + 1u, init);                      // H(i, 0), :83-86; kept while the lane is idle
+    int recv = 0;                                    // lane 0's first diag is H(0, 0) = 0
+    int bh = INT_MIN, rb = INT_MIN;
+    uint32_t bj = 0, rbj = 0, acc = 0;
+    const uint32_t steps = m + n - 1u;
+    uint32_t tnext = L.t[min(0u - l, m - 1u) & 0x3FFu];
+    for (uint32_t t = 0; t < steps; ++t) {
+        const int dg = recv;                          // H(i-1, j-1)
+        recv = wave_shr1(wmul(t + 1u, init), H);      // H(i-1, j); lane 0: row 0, :89-92
+        const uint32_t tb = tnext;
+        tnext = L.t[min(t + 1u - l, m - 1u) & 0x3FFu];  // next column's target byte (clamped, unused when idle)
+        const int j = (int)t - lane + 1;
+        uint32_t c = 0;
+        if (row && j >= 1 && j <= (int)m) {
+            const int diag = wadd(dg, qb == tb ? ma : mi);  // match_func, :20-23
+            const int left = wadd(H, tb == (uint32_t)'-' ? 0 : gap);
+            const int up = wadd(recv, upg);
+            int h = diag;
+            if (left > h) {
+                h = left;
+                c = 1;
+            }
+            if (up > h) {
+                h = up;
+                c = 2;
+            }
+            if (MODE == kLocal) {
+                if (h < 0) h = 0;  // :185
+                if (h == 0) c = 3;  // the walk stops here (:202)
+                if (h > bh) {       // :186, the first column keeps a tie
+                    bh = h;
+                    bj = (uint32_t)j;
+                }
+            }
+            if (MODE == kSemi && l == n - 1u && h > rb) {  // row n, :272-278
+                rb = h;
+                rbj = (uint32_t)j;
+            }
+            H = h;
+        }
+        acc |= c << (2u * (t & 15u));
+        if ((t & 15u) == 15u || t + 1u == steps) {
+            L.codes[(t >> 4) * kWave + l] = acc;
+            acc = 0;
+        }
+    }
+    PairOut o{0, 0, n, m, 0, 0};
+    if (MODE == kGlobal) {
+        o.score = rdlane(H, n - 1u);  // H(n, m)
+    } else if (MODE == kLocal) {
+        const int mx = wave_max(row ? bh : INT_MIN);
+        const int fl = first_lane(row && bh == mx);
+        o.score = mx;
+        o.gi = (uint32_t)fl + 1u;
+        o.gj = (uint32_t)rdlane((int)bj, (uint32_t)fl);
+        o.tb = o.gj + 1u;  // :197-199
+    } else {
+        // column m from row 0 (cost 0), strict '>' (:265-271), then row n (:272-278)
+        const int mx = wave_max(row ? H : INT_MIN);
+        int best = 0;
+        o.gi = 0;
+        o.gj = m;
+        if (mx > best) {
+            best = mx;
+            o.gi = (uint32_t)first_lane(row && H == mx) + 1u;
+        }
+        const int r = rdlane(rb, n - 1u);
+        if (r > best) {
+            best = r;
+            o.gi = n;
+            o.gj = (uint32_t)rdlane((int)rbj, n - 1u);
+        }
+        o.score = best;
+    }
+    if (!want) return o;
+    __syncthreads();  // the code dwords of every lane
+    // the walk, end to start (uniform; LDS broadcast reads), as runs (op | count << 2)
+    uint32_t nr = 0, op = 4u, cnt = 0;
+    auto push = [&](uint32_t o2, uint32_t k) {
+        if (o2 == op) {
+            cnt += k;
+        } else {
+            if (cnt) L.runs[nr++] = op | (cnt << 2);
+            op = o2;
+            cnt = k;
+        }
+    };
+    uint32_t i = o.gi, jj = o.gj;
+    if (MODE == kSemi && (jj != m || i != n)) {  // the trailing I / D of :306-315 end the string
+        if (i == n) push(1u, m - jj);
+        else if (jj == m) push(2u, n - i);
+    }
+    auto code_at = [&](uint32_t ci, uint32_t cj) {
+        const uint32_t st = cj + ci - 2u;
+        return (L.codes[(st >> 4) * kWave + (ci - 1u)] >> (2u * (st & 15u))) & 3u;
+    };
+    if (MODE == kLocal) {
+        while (i >= 1u && jj >= 1u) {  // cost > 0 (boundary cells cost 0)
+            const uint32_t c = code_at(i, jj);
+            if (c == 3u) break;
+            push(c, 1u);
+            i -= (c != 1u) ? 1u : 0u;
+            jj -= (c != 2u) ? 1u : 0u;
+        }
+    } else {
+        while (i > 0u || jj > 0u) {
+            if (i == 0u) {  // row 0: parent INSERT (:88-92)
+                push(1u, jj);
+                break;
+            }
+            if (jj == 0u) {  // column 0: parent DELETE (:82-86)
+                push(2u, i);
+                break;
+            }
+            const uint32_t c = code_at(i, jj);
+            push(c, 1u);
+            i -= (c != 1u) ? 1u : 0u;
+            jj -= (c != 2u) ? 1u : 0u;
+        }
+    }
+    if (cnt) L.runs[nr++] = op | (cnt << 2);
+    // RLE text, forward order = the runs in reverse, 64 runs per round
+    uint32_t used = 0;
+    if (nr == 0) {
+        if (lane == 0) {
+            L.text[0] = '1';
+            L.text[1] = '\0';
+        }
+        used = 2;
+    }
+    for (uint32_t base = 0; base < nr; base += 64u) {
+        const uint32_t f = base + l;
+        const bool act = f < nr;
+        const uint32_t v = act ? L.runs[nr - 1u - f] : 0u;
+        uint32_t c = v >> 2;
+        const uint32_t digits = 1u + (c >= 10u) + (c >= 100u) + (c >= 1000u) + (c >= 10000u);
+        const uint32_t len = act ? digits + 1u : 0u;
+        uint32_t incl = len;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, d, 64);
+            if (lane >= d) incl += y;
+        }
+        if (act) {
+            char* p = L.text + used + incl - len;
+            for (int d = (int)digits - 1; d >= 0; --d) {
+                p[d] = (char)('0' + c % 10u);
+                c /= 10u;
+            }
+            p[digits] = (char)((0x44494Du >> (8u * (v & 3u))) & 0xFFu);  // 'M', 'I', 'D'
+        }
+        used += (uint32_t)__shfl((int)incl, 63, 64);
+    }
+    __syncthreads();
+    for (uint32_t k = l; k < used; k += 64u) out_text[k] = L.text[k];
+    o.clen = used;
+    return o;
+}
+
 // One request of slot s: copy the bytes into HBM, fill + walk, results back.
 // The request header and the first KB of each sequence come in one round trip
 // over PCIe (lanes 0-5 the header words, the others query bytes; a second load
-// per lane the target); longer sequences follow in a second round.
+// per lane the target); longer sequences follow in a second round.  Small
+// pairs stay in LDS (serve_small).
 template <int MODE>
 __device__ __forceinline__ void serve_one(const ServeArgs& sa, uint32_t s, char* slot, uint32_t seq, int lane,
-                                          uint64_t t0) {
+                                          uint64_t t0, SmallLds& L) {
     ServeHdr* hd = reinterpret_cast<ServeHdr*>(slot);
     const uint32_t* req = reinterpret_cast<const uint32_t*>(slot);
     const FillArgs& fa = sa.fa;
@@ -439,6 +632,13 @@ __device__ __forceinline__ void serve_one(const ServeArgs& sa, uint32_t s, char*
     char* cslot = a.slots + (uint64_t)s * ((cigar_slot_bytes(kSrvQMax, kSrvTMax) + 255) & ~255ull);
     if (n > kSrvQMax || m > kSrvTMax) {
         status = TA_ERR_ARG;  // (the host never posts such a pair)
+    } else if (n >= 1 && m >= 1 && n <= kSmallQ && m <= kSmallT) {
+        if (lane >= 6 && lane < 10) *reinterpret_cast<uint4*>(L.q + 16u * (uint32_t)(lane - 6)) = qv;
+        *reinterpret_cast<uint4*>(L.t + 16u * (uint32_t)lane) = tv;
+        __syncthreads();
+        t1 = wall_clock64();
+        o = serve_small<MODE>(a, n, m, want, L, slot + kSrvCOff, lane);
+        t2 = wall_clock64();
     } else {
         if (lane >= 6) *reinterpret_cast<uint4*>(dq + 16u * (uint32_t)(lane - 6)) = qv;
         *reinterpret_cast<uint4*>(dt + 16u * (uint32_t)lane) = tv;
@@ -480,6 +680,7 @@ __global__ __launch_bounds__(kWave) void serve_kernel(ServeArgs sa) {
     const uint32_t s = blockIdx.x;
     char* slot = sa.host + (uint64_t)s * kSrvStride;
     const uint32_t* seqp = reinterpret_cast<const uint32_t*>(slot);
+    __shared__ SmallLds lds;
     // resume from the last finished request: one posted while no kernel ran is served now
     uint32_t last = (uint32_t)rdlane((int)(lane == 0 ? sys_load(&reinterpret_cast<const ServeHdr*>(slot)->done) : 0u), 0);
     uint32_t hb_last = 0;
@@ -492,7 +693,7 @@ __global__ __launch_bounds__(kWave) void serve_kernel(ServeArgs sa) {
                        hb = (uint32_t)rdlane((int)v, 2);
         if (seq != last) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the request's bytes were written before seq
-            serve_one<MODE>(sa, s, slot, seq, lane, wall_clock64());
+            serve_one<MODE>(sa, s, slot, seq, lane, wall_clock64(), lds);
             last = seq;
             t_hb = wall_clock64();
             continue;
