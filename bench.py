@@ -156,7 +156,10 @@ class Dist:
         self.dev_index = 0 if os.environ.get("TA_BENCH_ONE_GPU") == "1" else self.local_rank
         torch.cuda.set_device(self.dev_index)
         self.dev = torch.device("cuda", self.dev_index)
-        if self.world > 1:
+        # TA_BENCH_FORCE_DIST=1 (tests only): a world of one under torch.distributed.run still
+        # initialises the process group and gathers every step, which exercises the RCCL
+        # branch of ResultGather on a one-GPU box (two RCCL ranks cannot share one device)
+        if self.world > 1 or os.environ.get("TA_BENCH_FORCE_DIST") == "1":
             import torch.distributed as dist
 
             dist.init_process_group(self.backend, device_id=self.dev if self.backend == "nccl" else None)
@@ -598,7 +601,7 @@ def main_align(args, D):
 
         cells = full.qlen.astype(np.int64) * full.tlen.astype(np.int64)
         P_max = max(h - l for l, h in shard.range_split(cells, D.world))
-    gather = ResultGather(D, P_max, cigar) if D.world > 1 else None
+    gather = ResultGather(D, P_max, cigar) if D.dist else None
 
     def step():
         plan.run()
@@ -722,7 +725,7 @@ def main_align(args, D):
                        "mode": args.mode, "cigar": cigar, "cells_per_gpu": batch.cells, "cells_total": cells_job,
                        "parallelism": (f"one read set range-split by cells over {D.world} GPU(s)" if strong else
                                        f"pairs range-split over {D.world} GPU(s)")
-                       + (", RCCL all-gather of per-pair records and CIGAR bytes every step" if D.world > 1 else "")},
+                       + (", per-pair records and CIGAR bytes gathered to rank 0 every step (RCCL)" if D.world > 1 else "")},
             "fill_ms": round(fill_ms, 4), "traceback_ms": round(float(np.mean(tt)), 4) if cigar else None,
             "batch_latency_ms": round(fill_ms + (float(np.mean(tt)) if cigar else 0.0), 4),
             "chunks": plan.chunks, "workspace_gb": round(plan.workspace_bytes / 2**30, 2),

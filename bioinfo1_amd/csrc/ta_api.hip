@@ -34,6 +34,7 @@ struct ta_plan {
     uint32_t* d_fb = nullptr;  // packed-fill hand-back: [n_dual_pairs] list, then one counter per chunk
     uint32_t *d_flex_task_off = nullptr, *d_tickets = nullptr, *d_err = nullptr, *d_flex_tasks = nullptr;
     void* d_pout = nullptr;  // PassOut[2] per flex task
+    void* d_dpout = nullptr;  // PassOut[2] per (pass, dual couple) of one multi-pass chunk
 };
 
 namespace {
@@ -45,8 +46,16 @@ bool valid_type(int t) { return t == TA_GLOBAL || t == TA_LOCAL || t == TA_SEMI_
 // as zeros); goal cells, the hand-back list and the pass results are device-only.
 struct PlanOffs {
     uint64_t qlen, tlen, order, singles, duals, flexes, task_off, tasks, ptr_off, bnd_off, slot_off, err, tickets;
-    uint64_t goal_i, goal_j, fb, pout;
+    uint64_t goal_i, goal_j, fb, pout, dpout;
 };
+
+// PassOut[2] (24 bytes each) per (pass, couple) of the largest multi-pass dual chunk
+uint64_t dual_pout_bytes(const ta::Plan& h) {
+    uint64_t n = 0;
+    for (const auto& ch : h.chunks)
+        if (ch.dpasses > 1) n = std::max<uint64_t>(n, 2ull * ch.dcount * ch.dpasses);
+    return n * 24ull;
+}
 
 template <class T>
 uint64_t vbytes(const std::vector<T>& v) {
@@ -67,7 +76,7 @@ PlanOffs layout_uploaded(const ta::Plan& h, ta::BlockLayout& L) {
     o.bnd_off = L.add(vbytes(h.bnd_off));
     o.slot_off = L.add(vbytes(h.slot_off));
     o.err = L.add(4);
-    o.tickets = L.add(4ull * h.chunks.size());
+    o.tickets = L.add(8ull * h.chunks.size());  // per chunk: flex, then dual
     return o;
 }
 
@@ -76,6 +85,7 @@ void layout_scratch(const ta::Plan& h, ta::BlockLayout& L, PlanOffs& o) {
     o.goal_j = L.add(4ull * h.n_pairs);
     o.fb = L.add(4ull * (h.n_dual_pairs + h.chunks.size()));
     o.pout = L.add(h.flexes.empty() ? 0 : h.flex_task_off.back() * 48ull + 16);
+    o.dpout = L.add(dual_pout_bytes(h));
 }
 
 void pack(const ta::Plan& h, const PlanOffs& o, uint8_t* base) {
@@ -94,7 +104,7 @@ void pack(const ta::Plan& h, const PlanOffs& o, uint8_t* base) {
     put(o.bnd_off, h.bnd_off);
     put(o.slot_off, h.slot_off);
     std::memset(base + o.err, 0, 4);
-    std::memset(base + o.tickets, 0, 4ull * h.chunks.size());
+    std::memset(base + o.tickets, 0, 8ull * h.chunks.size());
 }
 
 void bind(ta_plan* pl, uint8_t* d, const PlanOffs& o) {
@@ -117,6 +127,7 @@ void bind(ta_plan* pl, uint8_t* d, const PlanOffs& o) {
     pl->d_goal_j = u32(o.goal_j);
     pl->d_fb = u32(o.fb);
     pl->d_pout = d + o.pout;
+    pl->d_dpout = d + o.dpout;
 }
 
 int check_args(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type) {
@@ -146,7 +157,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         // memory left there (traceback codes of a freed workspace, other
         // plans' records) must not survive: zero it (tag 0 is never valid)
         // before any kernel of this chunk is enqueued.
-        if (ch.fcount && ch.bnd_words) TA_HIP(ctx, hipMemsetAsync(d_bnd, 0, ch.bnd_words * 4ull, s));
+        if ((ch.fcount || ch.dpasses > 1) && ch.bnd_words) TA_HIP(ctx, hipMemsetAsync(d_bnd, 0, ch.bnd_words * 4ull, s));
         ta::FillArgs a{};
         a.order = pl->d_order;
         a.begin = ch.begin;
@@ -197,6 +208,14 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
                 d.count = ch.dcount;
                 d.fb_list = fb_list;
                 d.fb_count = fb_count;
+                if (ch.dpasses > 1) {  // one wave per (couple, pass), tickets pass-major
+                    d.ticket = pl->d_tickets + h.chunks.size() + c;
+                    d.n_tasks = ch.dcount * ch.dpasses;
+                    d.epoch = ++ctx->epoch & 0x3FFFFFFu;
+                    d.err = pl->d_err;
+                    d.pout = pl->d_dpout;
+                    TA_HIP(ctx, hipMemsetAsync(d.ticket, 0, 4, s));
+                }
                 if (ch.fcount) {  // beside the flexible fill: fork onto aux2 (after the counter reset), join below
                     TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
                     TA_HIP(ctx, hipStreamWaitEvent(ctx->aux2, ctx->ev_fork, 0));
@@ -301,9 +320,9 @@ struct LinearHostPlan final : ta_host::HostPlan {
     void bind(uint8_t* dev) override { ::bind(pl, dev, o); }
     int execute(const ta_device_io* io, hipStream_t s) override { return exec(pl, io, s, UINT32_MAX, true, true); }
     uint64_t slots_bytes() const override { return pl->h.slots_bytes; }
-    uint64_t err_offset() const override { return pl->h.flexes.empty() ? UINT64_MAX : o.err; }
+    uint64_t err_offset() const override { return pl->h.flexes.empty() && pl->h.duals.empty() ? UINT64_MAX : o.err; }
     const char* err_message() const override {
-        return "flexible fill: a pass hand-off poll timed out; results of this batch are invalid";
+        return "packed fill: a pass hand-off poll timed out; results of this batch are invalid";
     }
 };
 
@@ -469,13 +488,13 @@ int ta_plan_execute_traceback(ta_plan* pl, const ta_device_io* io, void* stream,
 
 int ta_plan_check(ta_plan* pl) {
     if (!pl) return TA_ERR_ARG;
-    if (pl->h.flexes.empty()) return TA_OK;
+    if (pl->h.flexes.empty() && pl->h.duals.empty()) return TA_OK;
     uint32_t err = 0;
     TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
     TA_HIP(pl->ctx, hipMemcpy(&err, pl->d_err, 4, hipMemcpyDeviceToHost));
     if (!err) return TA_OK;
     TA_HIP(pl->ctx, hipMemset(pl->d_err, 0, 4));
-    return fail(pl->ctx, TA_ERR_DEVICE, "flexible fill: a pass hand-off poll timed out; results of this plan are invalid");
+    return fail(pl->ctx, TA_ERR_DEVICE, "packed fill: a pass hand-off poll timed out; results of this plan are invalid");
 }
 
 int ta_compact_cigars(ta_context* ctx, uint32_t n_pairs, const char* cigar_slots, const uint64_t* cigar_start,

@@ -37,7 +37,41 @@ struct DualIo {
     const uint8_t* T[2];
     uint32_t* ptrs[2];
     int32_t* B;  // packed boundary row (pair A's allocation)
+    // One wave per (couple, pass) (multi-pass chunks): pass p's
+    // bottom row goes to 8-byte records tag << 32 | packed value in pair A's
+    // allocation (two buffers by pass parity), written with relaxed agent-scope
+    // stores; pass p + 1 polls 64 columns at a time until every record carries
+    // the tag it expects (the data is its own flag, as ta_flex.hip).  Null: the
+    // in-place row B of a wave that sweeps all passes itself.
+    uint64_t* rec_w;
+    const uint64_t* rec_r;
+    uint32_t tag_w, tag_r;
+    uint32_t* err;
 };
+
+typedef __attribute__((address_space(1))) unsigned long long gu64d;
+
+// columns 64k + lane + 1 of the previous pass's bottom row (packed pairs)
+__device__ __forceinline__ int dual_poll_chunk(const DualIo& io, uint32_t m, uint32_t k, int lane) {
+    const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+    const gu64d* r = (const gu64d*)(io.rec_r + j);
+    int v = 0;
+    for (uint32_t spins = 0;; ++spins) {
+        bool ok = true;
+        if (j <= m) {
+            const uint64_t x = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(x >> 32) == io.tag_r;
+            v = (int)(uint32_t)x;
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spins > (1u << 22)) {  // bounded: the kernel always ends
+            if (lane == 0) atomicOr(io.err, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return v;
+}
 
 // One pass of both pairs; see run_pass (ta_kernels.hip) for the shared structure.
 // M3 (local only): every value carries the offset `off` (local_max3_offset)
@@ -111,7 +145,8 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // the boundary row S(0, j) in pass 0, the previous pass's bottom row after.
     // UZ: minus dl, which the hand-off adds back in lane 0 too.
     auto top_chunk = [&](uint32_t c) -> int {
-        if (pass > 0) return (int)pk_sub((uint32_t)load_bchunk(io.B, m, c, lane), D2);
+        if (pass > 0)
+            return (int)pk_sub((uint32_t)(io.rec_r ? dual_poll_chunk(io, m, c, lane) : load_bchunk(io.B, m, c, lane)), D2);
         const int j = (int)(c * 64u + (uint32_t)lane + 1u);
         return (int)rep16(LOCAL ? off + zstep * j - dl : (init - ma) * j);
     };
@@ -235,7 +270,14 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jl, rowbest_j);
                 rowbest = pk_max(rowbest, v);
             }
-            if (has_next && (uint32_t)lane == nl - 1) io.B[j] = (int32_t)(UZ ? pk_sub(H2[R - 1], rep16(dl * lane)) : H2[R - 1]);
+            if (has_next && (uint32_t)lane == nl - 1) {
+                const uint32_t bv = UZ ? pk_sub(H2[R - 1], rep16(dl * lane)) : H2[R - 1];
+                if (io.rec_w)
+                    __hip_atomic_store((gu64d*)(io.rec_w + j), ((uint64_t)io.tag_w << 32) | bv, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    io.B[j] = (int32_t)bv;
+            }
         }
         if (CIGAR) {
             // per pair: [I rows 8-15, I rows 0-7, D rows 8-15, D rows 0-7] (ta_internal.h Code)
@@ -354,16 +396,41 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
 #ifndef TA_DUAL_WAVES
 #define TA_DUAL_WAVES 5
 #endif
+constexpr uint32_t kDualSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to the int32 fill
+
+// Chunks of multi-pass couples (a.ticket set) run one wave per (couple, pass):
+// ticket t is pass t / count of couple t % count (pass-major), so the pass a
+// wave polls belongs to a wave that took an earlier ticket and is running;
+// each wave writes its pass's PassOut and dual_combine_kernel folds them.
+// Otherwise one wave per couple sweeps its passes.
 template <int MODE, bool CIGAR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
-    const uint32_t widx = wave_id();
-    if (widx >= a.count) return;
+    uint32_t widx, p_only = 0;
+    const bool pipe = a.ticket != nullptr;
+    if (pipe) {
+        uint32_t tk = 0;
+        if (lane == 0) tk = atomicAdd(a.ticket, 1u);
+        tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+        if (tk >= a.n_tasks) return;
+        p_only = tk / a.count;
+        widx = tk - p_only * a.count;
+    } else {
+        widx = wave_id();
+        if (widx >= a.count) return;
+    }
     uint32_t p[2];
     p[0] = a.order[2 * (a.begin + widx)];
     p[1] = a.order[2 * (a.begin + widx) + 1];
     const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
+    const uint32_t passes = n_passes(n);
+    if (pipe && p_only >= passes) return;
+    PassOut* po = pipe ? static_cast<PassOut*>(a.pout) + 2ull * ((uint64_t)p_only * a.count + widx) : nullptr;
     DualIo io;
+    io.rec_w = nullptr;
+    io.rec_r = nullptr;
+    io.tag_w = io.tag_r = 0;
+    io.err = a.err;
     bool dash = false, qother = false;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -385,17 +452,40 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     // same workspace).
     if (__ballot(dash)) {
         if (lane == 0) {
-            // a self-coupled pair (p[0] == p[1], ta_planner.cpp) is handed back once:
-            // two int32 waves on one pair would share its in-place boundary row
-            const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
-            const uint32_t at = atomicAdd(a.fb_count, k);
-            a.fb_list[at] = p[0];
-            if (k == 2) a.fb_list[at + 1] = p[1];
+            if (!pipe || p_only == 0) {
+                // a self-coupled pair (p[0] == p[1], ta_planner.cpp) is handed back once:
+                // two int32 waves on one pair would share its in-place boundary row
+                const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
+                const uint32_t at = atomicAdd(a.fb_count, k);
+                a.fb_list[at] = p[0];
+                if (k == 2) a.fb_list[at + 1] = p[1];
+            }
+            if (pipe) {
+                po[0].i = kDualSkip;
+                po[1].i = kDualSkip;
+            }
         }
         return;
     }
-    const uint32_t passes = n_passes(n);
     io.B = (passes > 1) ? a.bnd + a.bnd_off[p[0]] : nullptr;
+    if (pipe) {
+        // tags never 0, unique per launch and pass (passes < 64: dual couples fit
+        // int16); the host zeroes the records before each launch
+        uint64_t* rec = reinterpret_cast<uint64_t*>(io.B);
+        const uint64_t rb = (uint64_t)m + 1;
+        io.rec_w = (p_only + 1 == passes) ? nullptr : rec + (p_only & 1u) * rb;
+        io.rec_r = p_only ? rec + ((p_only - 1u) & 1u) * rb : nullptr;
+        io.tag_w = a.epoch * 64u + p_only + 1u;
+        io.tag_r = a.epoch * 64u + p_only;
+        const bool last_pass = p_only + 1 == passes;
+        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, p_only, last_pass, lane)
+                              : dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, p_only, last_pass, lane);
+        if (lane == 0) {
+            po[0] = o.o[0];
+            po[1] = o.o[1];
+        }
+        return;
+    }
     int best_h[2], corner[2] = {0, 0};
     uint32_t best_i[2], best_j[2];
 #pragma unroll
@@ -453,6 +543,44 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
 
 inline dim3 dual_grid(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock); }
 
+// After a pipelined dual fill: fold each couple's per-pass results in pass
+// order (the upper pass wins ties; semi: row n after column m, :265-278;
+// global: the last pass's corner).
+template <int MODE>
+__global__ void dual_combine_kernel(FillArgs a) {
+    const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= a.count) return;
+    const PassOut* po = static_cast<const PassOut*>(a.pout);
+    if (po[2ull * w].i == kDualSkip) return;
+    const uint32_t n = a.qlen[a.order[2 * (a.begin + w)]], m = a.tlen[a.order[2 * (a.begin + w)]];
+    const uint32_t passes = n_passes(n);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+        const uint32_t p = a.order[2 * (a.begin + w) + h];
+        int best_h = (MODE == kSemi) ? 0 : INT_MIN, corner = 0;
+        uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
+        for (uint32_t k = 0; k < passes; ++k) {
+            const PassOut& o = po[2ull * ((uint64_t)k * a.count + w) + h];
+            if (MODE != kGlobal && o.h > best_h) {
+                best_h = o.h;
+                best_i = o.i;
+                best_j = o.j;
+            }
+            if (MODE == kSemi && k + 1 == passes && o.row_h > best_h) {
+                best_h = o.row_h;
+                best_i = n;
+                best_j = o.row_j;
+            }
+            if (MODE == kGlobal && k + 1 == passes) corner = o.corner;
+        }
+        if (h == 1 && p == a.order[2 * (a.begin + w)]) break;  // a pair coupled with itself
+        a.score[p] = (MODE == kGlobal) ? corner : best_h;
+        a.target_begin[p] = (MODE == kLocal) ? best_j + 1 : 0;
+        a.goal_i[p] = (MODE == kGlobal) ? n : best_i;
+        a.goal_j[p] = (MODE == kGlobal) ? m : best_j;
+    }
+}
+
 #endif  // TA_DUAL_MODE
 }  // namespace
 
@@ -460,8 +588,10 @@ inline dim3 dual_grid(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1)
 template <>
 hipError_t launch_dual_mode<TA_DUAL_MODE, (TA_DUAL_CIGAR != 0)>(const FillArgs& a, hipStream_t s) {
     if (!a.count) return hipSuccess;
-    hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, TA_DUAL_CIGAR != 0>), dual_grid(a.count), dim3(kBlock), 0, s,
-                       a);
+    hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, TA_DUAL_CIGAR != 0>), dual_grid(a.ticket ? a.n_tasks : a.count),
+                       dim3(kBlock), 0, s, a);
+    if (a.ticket)
+        hipLaunchKernelGGL(dual_combine_kernel<TA_DUAL_MODE>, dim3((a.count + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }
 #endif

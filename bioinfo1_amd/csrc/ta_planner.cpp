@@ -242,7 +242,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     };
     auto unit_waves = [&](size_t k) -> uint64_t {
         const Unit& u = units[k];
-        return u.kind == 2 ? n_passes(qlen[u.a]) : 1;  // flex: one wave per (couple, pass)
+        return u.kind ? n_passes(qlen[u.a]) : 1;  // packed fills: one wave per (couple, pass)
     };
     const std::vector<size_t> starts = chunk_starts(units.size(), budget_dw, wave_quantum, unit_codes, unit_waves);
     size_t next_cut = 1;
@@ -252,7 +252,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     auto open_chunk = [&]() {
         cur = Plan::Chunk{(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0,
                           (uint32_t)(pl.duals.size() / 2), 0, (uint32_t)(pl.flexes.size() / 2), 0,
-                          couples_before, 0, 0};
+                          couples_before, 0, 0, 0};
     };
     open_chunk();
     for (size_t k = 0; k < units.size(); ++k) {
@@ -275,6 +275,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
             uint64_t bw = bnd_words(qlen[x], tlen[x]);
             if (u.kind == 2 && h == 0 && n_passes(na) > 1)
                 bw = std::max<uint64_t>(bw, 8ull * ((uint64_t)std::max(ma, mb) + 1));
+            // dual: pair A holds the couple's packed hand-off records, 2 buffers x 8 bytes per column
+            if (u.kind == 1 && h == 0 && n_passes(na) > 1) bw = std::max<uint64_t>(bw, 4ull * ((uint64_t)ma + 1));
             bw += bw & 1;  // keep every region 8-byte aligned (64-bit hand-off records)
             cur.ptr_dwords += xd;
             cur.bnd_words += bw;
@@ -284,6 +286,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
             pl.duals.push_back(u.a);
             pl.duals.push_back(u.b);
             ++cur.dcount;
+            cur.dpasses = std::max(cur.dpasses, n_passes(na));
         } else if (u.kind == 2) {
             pl.flexes.push_back(u.a);
             pl.flexes.push_back(u.b);

@@ -58,6 +58,7 @@ struct Plan {
         uint32_t fbegin, fcount;  // flexible dual fill: pair couples
         uint32_t cbegin;          // couples (dual + flex) before this chunk: its slice of the hand-back list
         uint64_t ptr_dwords, bnd_words;
+        uint32_t dpasses;         // largest pass count of the dual couples (> 1: one wave per couple and pass)
     };
     std::vector<Chunk> chunks;
     uint32_t n_dual_pairs = 0;  // pairs in packed couples (dual + flex)

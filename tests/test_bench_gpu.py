@@ -40,3 +40,24 @@ def test_cfg2_two_ranks_gather():
                  "--no-cpu")
     assert out["n_gpus"] == 2 and out["scaling"] == "weak"
     assert out["gather"]["bit_exact"] and out["gather"]["pairs_gathered"] == 1200, out["gather"]
+
+
+def test_rccl_gather_world_one():
+    """The RCCL branch of ResultGather (gather on a side stream, then
+    point-to-point CIGAR bytes) with a world of one under
+    torch.distributed.run: the only RCCL run a one-GPU box allows."""
+    import socket
+
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    env = dict(os.environ, TA_BENCH_FORCE_DIST="1", HSA_ENABLE_IPC_MODE_LEGACY="0")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "1", "--dist-backend", "nccl", "--pairs", "600", "--steps", "2", "--warmup", "1",
+                        "--no-cpu", "--no-host", "--no-score-only"], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    g = out["gather"]
+    assert g["bit_exact"] and g["pairs_gathered"] == 600 and g["cigar_bytes"] > 0, g

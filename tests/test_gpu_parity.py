@@ -122,6 +122,9 @@ DUAL_FUZZ = [
     (1, (1, -1, -1), b"ACGT", [(1024, 1024), (1025, 700), (1500, 1500), (1900, 1900)], 24),
     (2, (1, -1, -1), b"AC", [(1024, 1024), (1025, 700), (1500, 1500), (2100, 900)], 24),
     (1, (1, 2, -3), b"AC", [(1017, 333), (2049, 64)], 12),
+    # multi-pass couples run one wave per (couple, pass); couples with '-' are handed back
+    (2, (2, -1, 2), b"AC-GT", [(2100, 1200), (1500, 800)], 16),
+    (0, (1, -1, -1), b"ACGTTTTTTTTTTTTTTTTTTTTTTTTTTTTTTTTT-", [(3100, 700), (1030, 1030)], 16),
 ]
 
 
