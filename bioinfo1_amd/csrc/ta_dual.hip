@@ -6,8 +6,9 @@
 // Each 32-bit register holds pair A in bits 15:0 and pair B in bits 31:16.
 // The stored value is not H itself but a biased S chosen so that the
 // diagonal candidate costs ONE v_pk_mad_i16 (e * (mi-ma) + S_diag, with
-// e = min(q ^ t, 1) per half) and the other two one v_pk_add each:
-//   global / semi:  S = H - ma*j
+// e = min(q ^ t, 1) per half) and the other two at most one v_pk_add each:
+//   global / semi:  S = H - ma*j + gap*(j - i)   (the up candidate is the
+//                   value above itself, the left one S + 2*gap - ma)
 //   local:          S = 16*H + (1 - 16*ma)*j - i
 //     (the -i term tags the row: within a step S - Zbase + 15 = 16H + 15 - r
 //      is the reference's row-major first-max key; the clamp H >= 0 becomes
@@ -90,8 +91,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     const int init = (MODE == kGlobal) ? gap : 0;
     const int zstep = 1 - 16 * ma;  // local: S(0, j) = zstep * j
     const uint32_t KD = rep16(LOCAL ? 16 * (mi - ma) : (mi - ma));
-    const uint32_t GL = rep16(LOCAL ? 16 * gap + zstep : gap - ma);  // left gain (no '-' in these targets)
-    const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : gap);  // up gain (no '-' in these queries)
+    // left gain (no '-' in these targets); global / semi: the up gain is 0 (the
+    // -gap*i term of S), so the left one carries gap twice
+    const uint32_t GL = rep16(LOCAL ? 16 * gap + zstep : 2 * gap - ma);
+    const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : 0);  // up gain (no '-' in these queries)
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16 (see pk_min_u16)
     const uint32_t Tmax = pass_steps(m);
@@ -114,10 +117,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
         if constexpr (CLS) q2[r] = i0 < n ? row_selector(io.Q[0][i0], io.Q[1][i0]) : row_selector(0, 0);
         else q2[r] = i0 < n ? ((uint32_t)io.Q[0][i0] | ((uint32_t)io.Q[1][i0] << 16)) : 0u;
-        H2[r] = rep16(LOCAL ? off - (int)(i0 + 1) + dl * lane : wmul(i0 + 1, init));  // S(i, 0)
+        H2[r] = rep16(LOCAL ? off - (int)(i0 + 1) + dl * lane : wmul(i0 + 1, init - gap));  // S(i, 0)
     }
     const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
-    uint32_t recv = rep16(LOCAL ? off - (int)ia + dl * lane : wmul(ia, init));
+    uint32_t recv = rep16(LOCAL ? off - (int)ia + dl * lane : wmul(ia, init - gap));
     uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
     const uint32_t nv_lane = (uint32_t)lane < nl - 1 ? R : ((uint32_t)lane == nl - 1 ? NV : 0);
     // Per-lane running values, both pairs packed, advanced once per step:
@@ -130,7 +133,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     int zu = off - (int)row_base - 1;  // UZ: the clamp base of row 0 in the lane frame (t = -1)
     const uint32_t ZS2 = rep16(zstep);
     uint32_t jj = rep16(-lane);
-    const uint32_t MA2 = rep16(ma);
+    const uint32_t MAG2 = rep16(ma - gap);
     // local: best key S - Zb = 16H - r (r = row in the stripe), -16 = no cell yet
     uint32_t bestK = rep16(-16), bestj = 0;
     uint32_t rowbest = rep16(-32768), rowbest_j = 0;  // semi: best of row n, its column
@@ -148,7 +151,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         if (pass > 0)
             return (int)pk_sub((uint32_t)(io.rec_r ? dual_poll_chunk(io, m, c, lane) : load_bchunk(io.B, m, c, lane)), D2);
         const int j = (int)(c * 64u + (uint32_t)lane + 1u);
-        return (int)rep16(LOCAL ? off + zstep * j - dl : (init - ma) * j);
+        return (int)rep16(LOCAL ? off + zstep * j - dl : (init - ma + gap) * j);
     };
     int bcur = top_chunk(0), bnext = top_chunk(1);
     const uint32_t steps = m + nl - 1;
@@ -217,7 +220,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 const uint32_t diag = dnext;
                 const uint32_t left = pk_add(old, GL);
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
-                const uint32_t up = pk_add(upv, GUG);
+                const uint32_t up = LOCAL ? pk_add(upv, GUG) : upv;
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv;
                 if constexpr (M3) hv = pk_max3_pos_bc<r & 1>(m1, up, W[r / 2]);  // clamp folded in, :185
@@ -262,11 +265,11 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                     bestK = pk_max(bestK, key);
                 }
             }
-            if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + ma*j, strict '>' (:271-278)
-                // j and ma*j of this lane's column, formed here rather than carried
-                // through the passes that never read them
+            if (MODE == kSemi && (NV != R || last_pass)) {  // row n: H = S + (ma-gap)*j + gap*n, strict '>' (:271-278)
+                // j of this lane's column, formed here rather than carried through
+                // the passes that never read it; + gap*n is added at the end
                 const uint32_t jl = rep16((int)t + 1 - lane);
-                const uint32_t v = pk_mad_i16(jl, MA2, H2[NV - 1]);
+                const uint32_t v = pk_mad_i16(jl, MAG2, H2[NV - 1]);
                 rowbest_j = bfi(half_mask(pk_sub_sat(rowbest, v)), jl, rowbest_j);
                 rowbest = pk_max(rowbest, v);
             }
@@ -325,12 +328,12 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             o.i = row_base + (uint32_t)fl * R + (uint32_t)(15 - (Kf & 15)) + 1;
             o.j = jf;
         } else if (MODE == kSemi) {
-            // column m: H = S + ma*m for every row, so S orders them
+            // column m: H = S + (ma-gap)*m + gap*i; first lane, then first row (:265-270)
             int cv = INT_MIN;
             uint32_t cr = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int sv = h ? hi16(H2[r]) : lo16(H2[r]);
+                const int sv = (h ? hi16(H2[r]) : lo16(H2[r])) + gap * (int)(row_base + (uint32_t)lane * R + r + 1);
                 if ((uint32_t)r < nv_lane && sv > cv) {
                     cv = sv;
                     cr = r;
@@ -338,11 +341,12 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             }
             const int mx = wave_max(cv);
             const int fl = first_lane(cv == mx && nv_lane > 0);
-            o.h = mx + ma * (int)m;
+            o.h = mx + (ma - gap) * (int)m;
             o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane((int)cr, fl) + 1;
             o.j = m;
             if (last_pass) {
-                o.row_h = rdlane(h ? hi16(rowbest) : lo16(rowbest), nl - 1);  // -32768: never set
+                const int rb = rdlane(h ? hi16(rowbest) : lo16(rowbest), nl - 1);
+                o.row_h = rb == -32768 ? INT_MIN : rb + gap * (int)n;  // -32768: never set
                 o.row_j = (uint32_t)rdlane((int)(h ? (rowbest_j >> 16) : (rowbest_j & 0xFFFFu)), nl - 1);
             }
         } else {
@@ -350,7 +354,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 int hv[R];
 #pragma unroll
                 for (int r = 0; r < R; ++r) hv[r] = h ? hi16(H2[r]) : lo16(H2[r]);
-                o.corner = rdlane(select_row<R>(hv, nrows - (nl - 1) * R - 1), nl - 1) + ma * (int)m;
+                o.corner = rdlane(select_row<R>(hv, nrows - (nl - 1) * R - 1), nl - 1) + (ma - gap) * (int)m + gap * (int)n;
             }
         }
     }

@@ -4,6 +4,7 @@
 #include "ta_planner.h"
 
 #include <algorithm>
+#include <climits>
 #include <cstdlib>
 #include <functional>
 #include <numeric>
@@ -47,10 +48,28 @@ bool fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {
         hi = 16 * hmax + std::max(0LL, z) * M + 32 * mag;
         lo = std::min(0LL, z) * M - N - 32 * mag;
         if (16 * hmax + 15 > 32767) return false;  // the argmax key 16H + 15 - r
-    } else {  // S = H - ma*j
-        const long long hmin = -(N + M) * mag;
-        hi = hmax + std::max(0LL, -(long long)ma) * M + 4 * mag;
-        lo = hmin - std::max(0LL, (long long)ma) * M - 4 * mag;
+    } else {
+        // S = H - ma*j + gap*(j - i) over the rows 0..n+15 (the last lane's padding
+        // rows) and columns 0..m.  H >= gap*min(i, j) (semi: gap steps from a 0
+        // boundary) or (i + j)*min(0, gap) (global), H <= hs*min(i, j) + (i + j)*gp.
+        // Both bounds and the bias are linear on either side of i = j, so their
+        // extremes lie on the vertices of the two triangles; the row-n values
+        // H - gap*n that the semi-global kernel also keeps packed are covered too.
+        const long long N1 = N + 16, g = gap, K = std::min(N1, M);
+        const long long hs = std::max({0LL, (long long)ma, (long long)mi}), gp = std::max(0LL, g);
+        const long long pts[5][2] = {{0, 0}, {N1, 0}, {0, M}, {N1, M}, {K, K}};
+        lo = LLONG_MAX;
+        hi = LLONG_MIN;
+        for (const auto& pt : pts) {
+            const long long i = pt[0], j = pt[1], mn = std::min(i, j);
+            const long long hl = (mode == kGlobal) ? (i + j) * std::min(0LL, g) : std::min(0LL, g) * mn;
+            const long long hh = hs * mn + (i + j) * gp;
+            const long long b = -(long long)ma * j + g * (j - i);
+            lo = std::min({lo, hl + b, hl - g * N1, hl - g * N});
+            hi = std::max({hi, hh + b, hh - g * N1, hh - g * N});
+        }
+        lo -= 8 * mag;
+        hi += 8 * mag;
     }
     return hi <= 32000 && lo >= -32000;
 }

@@ -79,6 +79,56 @@ int main(int argc, char** argv) {
                 }
             }
     }
-    std::printf("ok: %ld values (%ld max3-offset cases, %ld flex-local cases)\n", checked, dual_cases, flex_cases);
+    // fits_int16 (ta_planner.cpp) for the global / semi-global dual fill (ta_dual.hip):
+    // S = H - ma*j + gap*(j - i), every cell and candidate of rows up to n + 15, the
+    // semi row-n values H(n, j) - gap*n, all within int16 whenever it admits the shape
+    // (no '-' in either sequence: such couples go to the int32 fill)
+    long lin_cases = 0;
+    for (int it = 0; it < iters + 4; ++it) {
+        const uint32_t big = (it % 10 == 0) ? 3000 : 90;
+        uint32_t n = 1 + rng() % big, m = 1 + rng() % big;
+        int ma = (int)(rng() % 9) - 2, mi = (int)(rng() % 9) - 6, gap = (int)(rng() % 7) - 4;
+        int mode = (it & 1) ? ta::kGlobal : ta::kSemi;
+        if (it >= iters) {  // config 5's shape and scoring, and the largest shapes the bound admits
+            const uint32_t shapes[4][2] = {{10000, 10000}, {10000, 10000}, {15000, 9000}, {9000, 15000}};
+            n = shapes[it - iters][0];
+            m = shapes[it - iters][1];
+            ma = 1, mi = -1, gap = -1;
+            mode = (it - iters) == 1 ? ta::kGlobal : ta::kSemi;
+        }
+        if (!ta::fits_int16(mode, n, m, ma, mi, gap)) continue;
+        ++lin_cases;
+        const int na = 2 + rng() % 4;
+        const char alpha[] = "ACGTN";
+        std::string q(n + 16, 'A'), t(m, 'A');
+        for (auto& c : q) c = alpha[rng() % na];
+        for (auto& c : t) c = alpha[rng() % na];
+        const uint32_t N = n + 15;
+        const long init = mode == ta::kGlobal ? gap : 0;
+        std::vector<long> H((N + 1) * (m + 1), 0);
+        auto at = [&](uint32_t i, uint32_t j) -> long& { return H[(size_t)i * (m + 1) + j]; };
+        for (uint32_t i = 0; i <= N; ++i) at(i, 0) = init * (long)i;
+        for (uint32_t j = 0; j <= m; ++j) at(0, j) = init * (long)j;
+        auto bad = [&](long v, const char* what, uint32_t i, uint32_t j) {
+            ++checked;
+            if (v >= -32768 && v <= 32767) return false;
+            std::printf("fits_int16 violated (%s): mode=%d n=%u m=%u sc=%d,%d,%d i=%u j=%u v=%ld\n", what, mode, n, m, ma,
+                        mi, gap, i, j, v);
+            return true;
+        };
+        for (uint32_t i = 1; i <= N; ++i)
+            for (uint32_t j = 1; j <= m; ++j) {
+                const long d = at(i - 1, j - 1) + (q[i - 1] == t[j - 1] ? ma : mi);
+                const long l = at(i, j - 1) + gap, u = at(i - 1, j) + gap;
+                const long h = std::max({d, l, u});
+                at(i, j) = h;
+                const long b = -(long)ma * j + (long)gap * ((long)j - (long)i);
+                for (long cand : {d, l, u, h})
+                    if (bad(cand + b, "cell", i, j)) return 1;
+                if (mode == ta::kSemi && i == n && bad(h - (long)gap * n, "row n", i, j)) return 1;
+            }
+    }
+    std::printf("ok: %ld values (%ld max3-offset cases, %ld flex-local cases, %ld global/semi dual cases)\n", checked,
+                dual_cases, flex_cases, lin_cases);
     return 0;
 }
