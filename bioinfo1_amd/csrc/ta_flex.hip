@@ -6,7 +6,9 @@
 //
 // What differs from dual_pass (ta_dual.hip):
 //  * Wave-uniform rebasing.  The stored value is V = S - O with S = H - ma*j
-//    and O a per-pair wave-uniform int32 offset.  Every 64 steps all lanes
+//    (global / semi: S = H - ma*j + gap*(j - i), so that the up candidate is
+//    the value above itself, as ta_dual.hip) and O a per-pair wave-uniform
+//    int32 offset.  Every 64 steps all lanes
 //    subtract the same packed value from all their cells (O absorbs it), so
 //    values exchanged between lanes need no conversion.  In a linear-gap DP
 //    adjacent cells differ by at most max|score| + |gap|, so
@@ -104,10 +106,12 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     constexpr int R = kRows;
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const int init = (MODE == kGlobal) ? gap : 0;
+    constexpr bool LOC = MODE == kLocal;
+    const int rowb = LOC ? 0 : gap;  // global / semi: the -gap*i term of S (none in local)
     const uint32_t KD = rep16(mi - ma);
-    const int glg = gap - ma;  // left gain, target byte != '-'
-    const int gld = -ma;       // left gain, target byte == '-'
-    const uint32_t GUG = rep16(gap);
+    const int glg = gap - ma + rowb;  // left gain, target byte != '-'
+    const int gld = -ma + rowb;       // left gain, target byte == '-'
+    const uint32_t GUG = rep16(gap - rowb);  // up gain (0 in global / semi)
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16
     const uint32_t M = max(io.m[0], io.m[1]);
@@ -126,16 +130,16 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     const int amag = max(max(abs(ma), abs(mi)), abs(gap));
     const int C0 = LOCAL ? 64 * abs(ma) + 16 * amag + 64 : 0;
     // offsets: S(i, 0) = i * init, so start from the pass's first row
-    int O[2] = {wmul(row_base, init) - C0, wmul(row_base, init) - C0};
+    int O[2] = {wmul(row_base, init - rowb) - C0, wmul(row_base, init - rowb) - C0};
     uint32_t q2[R], H2[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) {
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
         const uint32_t qa = i0 < io.n[0] ? (uint32_t)io.Q[0][i0] : 0u, qb = i0 < io.n[1] ? (uint32_t)io.Q[1][i0] : 0u;
         q2[r] = CLS ? row_selector(qa, qb) : (qa | (qb << 16));
-        H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init) + C0);  // S(i, 0) - O
+        H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init - rowb) + C0);  // S(i, 0) - O
     }
-    uint32_t recv = rep16(wmul((uint32_t)lane * R, init) + C0);
+    uint32_t recv = rep16(wmul((uint32_t)lane * R, init - rowb) + C0);
     uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
     // local: clamp base Z = -ma*j - O per half (j = -lane before step 0), ma*j
     // (int32), the running best key 16*H + 15 - r and its column per pair
@@ -197,7 +201,8 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             int cv = INT_MIN, cr = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int v = (h ? sext_hi(H2[r]) : sext_lo(H2[r])) + oh;
+                // H - (ma - gap)*m_h: S plus the row term gap*i
+                const int v = (h ? sext_hi(H2[r]) : sext_lo(H2[r])) + oh + rowb * (int)(row_base + (uint32_t)lane * R + r + 1);
                 if ((uint32_t)r < nv && v > cv) {
                     cv = v;
                     cr = r;
@@ -206,14 +211,14 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             capv[h] = cv;
             capr[h] = cr;
         } else {
-            capv[h] = (h ? sext_hi(H2[NV - 1]) : sext_lo(H2[NV - 1])) + oh;
+            capv[h] = (h ? sext_hi(H2[NV - 1]) : sext_lo(H2[NV - 1])) + oh + rowb * (int)io.n[h];  // row n_h
         }
     };
     auto step = [&](uint32_t t, auto masked_tag) {
         constexpr bool MASKED = decltype(masked_tag)::value;
         uint32_t top;
         if (pass == 0) {
-            const int s0 = (init - ma) * (int)(t + 1);  // S(0, j)
+            const int s0 = (init - ma + rowb) * (int)(t + 1);  // S(0, j)
             top = ((uint32_t)(s0 - O[0]) & 0xFFFFu) | ((uint32_t)(s0 - O[1]) << 16);
         } else {
             const int ba = rdlane(bcur[0], t & 63u), bb = rdlane(bcur[1], t & 63u);
@@ -259,7 +264,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 const uint32_t diag = dnext;
                 const uint32_t left = pk_add(old, GL);
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
-                const uint32_t up = pk_add(upv, GUG);
+                const uint32_t up = LOC ? pk_add(upv, GUG) : upv;
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv;
                 if constexpr (LOCAL) hv = pk_max3_pos(m1, up, Z);  // clamp folded in, :185
@@ -304,7 +309,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             if (MODE == kSemi && last_pass) {  // row n of each pair: H = S + ma*j, columns <= m_h, strict '>'
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    const int v = (h ? sext_hi(H2[NV - 1]) : sext_lo(H2[NV - 1])) + O[h] + ma * j;
+                    const int v = (h ? sext_hi(H2[NV - 1]) : sext_lo(H2[NV - 1])) + O[h] + (ma - rowb) * j + rowb * (int)io.n[h];
                     const bool better = j <= (int)io.m[h] && v > rb[h];
                     rb[h] = better ? v : rb[h];
                     rbj[h] = better ? (uint32_t)j : rbj[h];
@@ -369,7 +374,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             const int mx = wave_max(capv[h]);
             const int fl = first_lane(capv[h] == mx && capv[h] != INT_MIN);
             if (mx != INT_MIN) {
-                o.h = mx + ma * (int)io.m[h];
+                o.h = mx + (ma - rowb) * (int)io.m[h];
                 o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane(capr[h], fl) + 1;
                 o.j = io.m[h];
             }
@@ -378,7 +383,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 o.row_j = (uint32_t)rdlane((int)rbj[h], nlh[h] - 1);
             }
         } else if (last_pass) {
-            o.corner = rdlane(capv[h], nlh[h] - 1) + ma * (int)io.m[h];
+            o.corner = rdlane(capv[h], nlh[h] - 1) + (ma - rowb) * (int)io.m[h];
         }
     }
     return out;

@@ -13,7 +13,10 @@ namespace ta {
 
 // The flexible fill keeps V = S - O within a wave's span: 1,024 rows + 2 x 64
 // columns of cells whose neighbours differ by at most |score| + |gap| <= 2*mag
-// (plus the 64-step drift between rebases).
+// (plus the 64-step drift between rebases).  Global / semi keep S = H - ma*j +
+// gap*(j - i): a vertical step of S lies in [0, hs - 2*gap] (H moves by
+// [gap, hs - gap] down a column) and a horizontal one within 4*mag, so the span
+// is at most (3*1024 + 8*64 + 8)*mag -- inside the same bound for mag <= 6.
 // Local mode also ranks a column's 16 rows by 16 * (V_r - V_0) + 15 - r,
 // within 16 * 15 * 2 * mag.
 bool flex_fits(int mode, int ma, int mi, int gap) {
