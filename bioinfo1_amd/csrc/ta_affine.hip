@@ -544,7 +544,10 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
     const int OX = O + X;
     const int K = abs(O) + abs(X) + 2;  // E(i,0) = H(i,0) - K, F(0,j) = H(0,j) - K
     const uint32_t KD = rep16(mi - ma);
-    const uint32_t GOQ = rep16(OX), GEQ = rep16(X);  // vertical (no '-' in these queries)
+    // Values are S = V - ma*j + X*(j - i) (V = H, E or F): the vertical extension
+    // fe = F above (no add), the vertical open H above + O; horizontal gains carry
+    // X twice.  No '-' in these queries.
+    const uint32_t GOQ = rep16(O);
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16 (ta_packed.h)
     const uint32_t Tmax = pass_steps(m);
@@ -560,16 +563,16 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;  // row i0 + 1
         if constexpr (CLS) q2[r] = i0 < n ? row_selector(Q[0][i0], Q[1][i0]) : row_selector(0, 0);
         else q2[r] = i0 < n ? ((uint32_t)Q[0][i0] | ((uint32_t)Q[1][i0] << 16)) : 0u;
-        const int h0 = (MODE == kGlobal) ? O + (int)(i0 + 1) * X : 0;  // H(i, 0)
+        const int h0 = ((MODE == kGlobal) ? O + (int)(i0 + 1) * X : 0) - X * (int)(i0 + 1);  // S of H(i, 0)
         H2[r] = rep16(h0);
         E2[r] = rep16(h0 - K);
     }
     const uint32_t ia = row_base + (uint32_t)lane * R;  // row above the stripe
-    uint32_t recvH = rep16((MODE == kGlobal && ia) ? O + (int)ia * X : 0);  // H(ia, 0)
+    uint32_t recvH = rep16(((MODE == kGlobal && ia) ? O + (int)ia * X : 0) - X * (int)ia);  // S of H(ia, 0)
     uint32_t recvF = 0, Flast = 0;
     uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
-    uint32_t maj = rep16(-ma * lane);  // ma*j at t = -1 (semi: row n holds H = S + ma*j)
-    const uint32_t MA2 = rep16(ma);
+    uint32_t maj = rep16(-(ma - X) * lane);  // (ma - X)*j at t = -1 (semi: row n holds H = S + (ma - X)*j + X*n)
+    const uint32_t MA2 = rep16(ma - X);
     uint32_t jj = rep16(-lane);
     uint32_t rowbest = rep16(-32768), rowbest_j = 0;
 
@@ -602,7 +605,7 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
         uint32_t topH, topF;
         if (pass == 0) {  // row 0 (:89-92 with an affine gap): H(0,j) - ma*j; F(0,j) = -inf stand-in
             const int jt = (int)t + 1;
-            const int h0 = ((MODE == kGlobal) ? O + jt * X : 0) - ma * jt;
+            const int h0 = ((MODE == kGlobal) ? O + jt * X : 0) - ma * jt + X * jt;
             topH = rep16(h0);
             topF = rep16(h0 - K);
         } else {
@@ -630,11 +633,11 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)m));
         uint32_t ax0 = 0, ax1 = 0, ay0 = 0, ay1 = 0;
         if (active) {
-            uint32_t GOT = rep16(OX - ma), GET = rep16(X - ma);  // horizontal, biased
-            if (tdash) {
+            uint32_t GOT = rep16(OX + X - ma), GET = rep16(2 * X - ma);  // horizontal, biased
+            if (tdash) {  // a '-' target byte: the horizontal step is free
                 const bool da = (tc2 & 0xFFFFu) == '-', db = (tc2 >> 16) == '-';
-                GOT = ((uint32_t)(da ? -ma : OX - ma) & 0xFFFFu) | ((uint32_t)(db ? -ma : OX - ma) << 16);
-                GET = ((uint32_t)(da ? -ma : X - ma) & 0xFFFFu) | ((uint32_t)(db ? -ma : X - ma) << 16);
+                GOT = ((uint32_t)(da ? X - ma : OX + X - ma) & 0xFFFFu) | ((uint32_t)(db ? X - ma : OX + X - ma) << 16);
+                GET = ((uint32_t)(da ? X - ma : 2 * X - ma) & 0xFFFFu) | ((uint32_t)(db ? X - ma : 2 * X - ma) << 16);
             }
             auto e_of = [&](int r) {  // 0 on a match, 1 otherwise
                 if constexpr (CLS) return mismatch_flags(tA, tB, q2[r]);
@@ -649,7 +652,7 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
                 const uint32_t eo = pk_add(old, GOT), ee = pk_add(E2[r], GET);
                 const uint32_t e = pk_max(eo, ee);
-                const uint32_t fo = pk_add(upH, GOQ), fe = pk_add(upF, GEQ);
+                const uint32_t fo = pk_add(upH, GOQ), fe = upF;
                 const uint32_t f = pk_max(fo, fe);
                 const uint32_t m1 = pk_max(diag, e);
                 const uint32_t h = pk_max(m1, f);
@@ -712,12 +715,12 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
         PassOut& o = out[h];
         o = PassOut{INT_MIN, 0, 0, INT_MIN, 0, 0};
         if (MODE == kSemi) {
-            // column m: H = S + ma*m for every row, so S orders them; first lane, then first row (:265-270)
+            // column m: H = S + (ma - X)*m + X*i; first lane, then first row (:265-270)
             int cv = INT_MIN;
             uint32_t cr = 0;
 #pragma unroll
             for (int r = 0; r < R; ++r) {
-                const int sv = h ? hi16(H2[r]) : lo16(H2[r]);
+                const int sv = (h ? hi16(H2[r]) : lo16(H2[r])) + X * (int)(row_base + (uint32_t)lane * R + r + 1);
                 if ((uint32_t)r < nv_lane && sv > cv) {
                     cv = sv;
                     cr = r;
@@ -725,18 +728,19 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
             }
             const int mx = wave_max(cv);
             const int fl = first_lane(cv == mx && nv_lane > 0);
-            o.h = mx + ma * (int)m;
+            o.h = mx + (ma - X) * (int)m;
             o.i = row_base + (uint32_t)fl * R + (uint32_t)rdlane((int)cr, fl) + 1;
             o.j = m;
             if (last_pass) {
-                o.row_h = rdlane(h ? hi16(rowbest) : lo16(rowbest), nl - 1);  // -32768: never set
+                const int rb = rdlane(h ? hi16(rowbest) : lo16(rowbest), nl - 1);
+                o.row_h = rb == -32768 ? INT_MIN : rb + X * (int)n;  // -32768: never set
                 o.row_j = (uint32_t)rdlane((int)(h ? (rowbest_j >> 16) : (rowbest_j & 0xFFFFu)), nl - 1);
             }
         } else if (last_pass) {
             int hv[R];
 #pragma unroll
             for (int r = 0; r < R; ++r) hv[r] = h ? hi16(H2[r]) : lo16(H2[r]);
-            o.corner = rdlane(select_row<R>(hv, nrows - (nl - 1) * R - 1), nl - 1) + ma * (int)m;
+            o.corner = rdlane(select_row<R>(hv, nrows - (nl - 1) * R - 1), nl - 1) + (ma - X) * (int)m + X * (int)n;
         }
     }
 }

@@ -77,22 +77,38 @@ bool fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {
     return hi <= 32000 && lo >= -32000;
 }
 
-// Every packed value of aff_dual_pass within int16, with margins: H from the
-// diagonal path below / any path above, E and F within one gap step of H, the
-// bias -ma*j, the -inf stand-ins (H - K) and one more step of candidates.
+// Every packed value of aff_dual_pass within int16, with margins.  The kernel
+// keeps S = V - ma*j + X*(j - i) for V = H, E, F.  Per cell (i, j), rows up to
+// n + 15 (the last lane's padding rows):
+//   H >= min(0, O + X*min(i, j))            semi (a gap run from a 0 boundary;
+//        (O + X*max(i, j) when X > 0)         0 on the boundary itself)
+//   H >= 2*min(0, O) + (i + j)*min(0, X)    global (down the column, then right)
+//   H <= hs*min(i, j) + (i + j)*(max(0, O) + max(0, X))
+// E and F lie within one gap step (|O| + |X|) of an H, the -inf stand-ins are
+// H - K, candidates one more step.  The lower bounds are concave and the upper
+// one linear on either side of i = j, so their extremes over the grid lie on
+// the vertices of the two triangles; the semi row-n values H - X*n are
+// covered too.
 bool affine_fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int open, int ext) {
     if (mode == kLocal || n == 0 || m == 0) return false;
-    const long long N = n, M = m, mn = std::min(N, M), mx = std::max(N, M);
-    const long long lo_s = std::min({0LL, (long long)ma, (long long)mi});
-    const long long hi_s = std::max({0LL, (long long)ma, (long long)mi});
-    long long hlo = mn * lo_s;
-    if (mode == kGlobal) hlo += std::min(0LL, (long long)open) + mx * std::min(0LL, (long long)ext);
-    const long long hhi = mn * hi_s + (N + M) * (std::max(0LL, (long long)open) + std::max(0LL, (long long)ext));
-    const long long k = std::llabs(open) + std::llabs(ext) + 2;
+    const long long N = n, N1 = N + 16, M = m, O = open, X = ext;
+    const long long hs = std::max({0LL, (long long)ma, (long long)mi});
+    const long long gp = std::max(0LL, O) + std::max(0LL, X);
+    const long long k = std::llabs(O) + std::llabs(X) + 2;
     const long long marg = 2 * k + 2 * std::llabs(ma) + std::llabs(mi) + 8;
-    const long long slo = hlo - std::max(0LL, (long long)ma) * M - marg;
-    const long long shi = hhi + std::max(0LL, -(long long)ma) * M + marg;
-    return slo >= -32000 && shi <= 32000;
+    const long long K = std::min(N1, M);
+    const long long pts[5][2] = {{0, 0}, {N1, 0}, {0, M}, {N1, M}, {K, K}};
+    long long lo = LLONG_MAX, hi = LLONG_MIN;
+    for (const auto& pt : pts) {
+        const long long i = pt[0], j = pt[1], mn = std::min(i, j), mx = std::max(i, j);
+        const long long hl = (mode == kGlobal) ? 2 * std::min(0LL, O) + (i + j) * std::min(0LL, X)
+                                               : std::min(0LL, O + X * (X <= 0 ? mn : mx));
+        const long long hh = hs * mn + (i + j) * gp;
+        const long long b = -(long long)ma * j + X * (j - i);
+        lo = std::min({lo, hl + b, hl - X * N});
+        hi = std::max({hi, hh + b, hh - X * N});
+    }
+    return lo - marg >= -32000 && hi + marg <= 32000;
 }
 
 namespace {

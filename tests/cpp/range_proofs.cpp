@@ -128,7 +128,67 @@ int main(int argc, char** argv) {
                 if (mode == ta::kSemi && i == n && bad(h - (long)gap * n, "row n", i, j)) return 1;
             }
     }
-    std::printf("ok: %ld values (%ld max3-offset cases, %ld flex-local cases, %ld global/semi dual cases)\n", checked,
-                dual_cases, flex_cases, lin_cases);
+    // affine_fits_int16 (ta_planner.cpp) for the packed affine fill (ta_affine.hip):
+    // S = V - ma*j + X*(j - i) for V = H, E, F and every candidate (diag, E open /
+    // extend, F open / extend), the -inf stand-ins H - K, rows up to n + 15, the semi
+    // row-n values H - X*n; rolling rows (config 5's 10k x 10k shape included)
+    long aff_cases = 0;
+    for (int it = 0; it < iters / 2 + 2; ++it) {
+        const uint32_t big = (it % 10 == 0) ? 3000 : 90;
+        uint32_t n = 1 + rng() % big, m = 1 + rng() % big;
+        int ma = (int)(rng() % 9) - 2, mi = (int)(rng() % 9) - 6, O = (int)(rng() % 9) - 5, X = (int)(rng() % 5) - 3;
+        int mode = (it & 1) ? ta::kGlobal : ta::kSemi;
+        if (it >= iters / 2) {
+            n = m = 10000;
+            ma = 1, mi = -1, O = -2, X = -1;
+            mode = (it - iters / 2) ? ta::kGlobal : ta::kSemi;
+        }
+        if (!ta::affine_fits_int16(mode, n, m, ma, mi, O, X)) continue;
+        ++aff_cases;
+        const int na = 2 + rng() % 4;
+        const char alpha[] = "ACGTN";
+        std::string q(n + 16, 'A'), t(m, 'A');
+        for (auto& c : q) c = alpha[rng() % na];
+        for (auto& c : t) c = alpha[rng() % na];
+        const uint32_t N = n + 15;
+        const long K = std::labs(O) + std::labs(X) + 2;
+        std::vector<long> Hp(m + 1), Fp(m + 1), Hc(m + 1), Fc(m + 1);
+        auto h0 = [&](long i) { return mode == ta::kGlobal && i ? O + i * X : 0L; };
+        for (uint32_t j = 0; j <= m; ++j) {
+            Hp[j] = h0(j);  // row 0 (global: O + j*X)
+            Fp[j] = Hp[j] - K;
+        }
+        auto bad = [&](long v, const char* what, long i, long j) {
+            ++checked;
+            if (v >= -32768 && v <= 32767) return false;
+            std::printf("affine_fits_int16 violated (%s): mode=%d n=%u m=%u sc=%d,%d,%d,%d i=%ld j=%ld v=%ld\n", what,
+                        mode, n, m, ma, mi, O, X, i, j, v);
+            return true;
+        };
+        for (uint32_t i = 1; i <= N; ++i) {
+            Hc[0] = h0(i);
+            long E = Hc[0] - K;
+            Fc[0] = Hc[0] - K;
+            if (bad(Hc[0] - (long)X * i, "column 0", i, 0) || bad(E - (long)X * i, "column 0 E", i, 0)) return 1;
+            for (uint32_t j = 1; j <= m; ++j) {
+                const long b = -(long)ma * j + (long)X * ((long)j - (long)i);
+                const long d = Hp[j - 1] + (q[i - 1] == t[j - 1] ? ma : mi);
+                const long eo = Hc[j - 1] + O + X, ee = E + X;
+                const long fo = Hp[j] + O + X, fe = Fp[j] + X;
+                E = std::max(eo, ee);
+                const long F = std::max(fo, fe);
+                const long h = std::max({d, E, F});
+                Hc[j] = h;
+                Fc[j] = F;
+                for (long v : {d, eo, ee, fo, fe, E, F, h, h - K})
+                    if (bad(v + b, "cell", i, j)) return 1;
+                if (mode == ta::kSemi && i == n && bad(h - (long)X * n, "row n", i, j)) return 1;
+            }
+            std::swap(Hp, Hc);
+            std::swap(Fp, Fc);
+        }
+    }
+    std::printf("ok: %ld values (%ld max3-offset cases, %ld flex-local cases, %ld global/semi dual cases, %ld affine "
+                "cases)\n", checked, dual_cases, flex_cases, lin_cases, aff_cases);
     return 0;
 }
