@@ -453,21 +453,32 @@ class DevicePlan:
         if r != TA_OK:
             _raise(r, self._ctx)
 
-    def compact_cigars(self):
+    def compact_cigars(self, out=None):
         """The CIGARs packed back to back on the device (ta_compact_cigars on
         the current stream): returns (bytes uint8 tensor, int64 offsets
-        tensor [P+1]) -- what a rank hands to an RCCL gather."""
+        tensor [P+1]) -- what a rank hands to an RCCL gather.  ``out``: a
+        (bytes, offsets) pair from compact_buffers() to fill instead of fresh
+        tensors (a pipeline reusing them per slot)."""
         torch = self.torch
         lens = self.cigar_len.to(torch.int64)
-        off = torch.zeros(self.P + 1, dtype=torch.int64, device=self.dev)
+        if out is None:
+            off = torch.zeros(self.P + 1, dtype=torch.int64, device=self.dev)
+            # a device-side bound keeps this free of host syncs: every CIGAR fits its slot
+            dst = torch.empty(max(self.slots_bytes, 1), dtype=torch.uint8, device=self.dev)
+        else:
+            dst, off = out
         torch.cumsum(lens, 0, out=off[1:])
-        # a device-side bound keeps this free of host syncs: every CIGAR fits its slot
-        dst = torch.empty(max(self.slots_bytes, 1), dtype=torch.uint8, device=self.dev)
         r = lib().ta_compact_cigars(self._ctx, self.P, self.slots.data_ptr(), self.cigar_start.data_ptr(),
                                     self.cigar_len.data_ptr(), off.data_ptr(), dst.data_ptr(), self._stream())
         if r != TA_OK:
             _raise(r, self._ctx)
         return dst, off
+
+    def compact_buffers(self):
+        """Buffers for compact_cigars(out=...): (bytes, offsets with offsets[0] = 0)."""
+        torch = self.torch
+        return (torch.empty(max(self.slots_bytes, 1), dtype=torch.uint8, device=self.dev),
+                torch.zeros(self.P + 1, dtype=torch.int64, device=self.dev))
 
     def pair_chunks(self) -> np.ndarray:
         """uint32 [P]: the chunk each pair ran in (ta_plan_pair_chunks)."""
@@ -578,10 +589,12 @@ class HostPipeline:
 
     Two DevicePlans alternate (double-buffered device inputs and outputs); they
     share the aligner's context, so their kernels run one after the other.  Step
-    k enqueues its upload and kernels, then waits for step k-1's records (12
-    bytes per pair; step k-1's kernels are done, step k's already queued behind
-    them) and posts the download of exactly step k-1's CIGAR bytes, ahead of
-    step k's records."""
+    k enqueues its upload and kernels, then waits for step k-1's kernels (step
+    k's are already queued behind them) and downloads step k-1's records (12
+    bytes per pair) and exactly its CIGAR bytes.  Every copy is posted only
+    once its data is ready: a copy enqueued ahead of its data (waiting on an
+    event) holds its DMA engine, and an upload queued behind it then waits for
+    a whole plan (measured: a 0.45 ms bubble every other step)."""
 
     def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, workspace_budget=0):
         import torch
@@ -593,12 +606,15 @@ class HostPipeline:
         self.dev = dev
         qb = batch.qbytes if batch.qbytes.size else np.zeros(1, np.uint8)
         tb = batch.tbytes if batch.tbytes.size else np.zeros(1, np.uint8)
-        self.h_q = torch.from_numpy(np.ascontiguousarray(qb)).pin_memory()
-        self.h_t = torch.from_numpy(np.ascontiguousarray(tb)).pin_memory()
+        # query and target bytes in one pinned buffer and one device buffer per
+        # slot: one H2D copy per step
+        nq = int(qb.size)
+        self.h_qt = torch.from_numpy(np.concatenate([np.ascontiguousarray(qb), np.ascontiguousarray(tb)])).pin_memory()
         qoff = torch.from_numpy(batch.qoff.view(np.int64).copy()).to(dev)
         toff = torch.from_numpy(batch.toff.view(np.int64).copy()).to(dev)
-        self.d_q = [torch.empty_like(self.h_q, device=dev) for _ in range(2)]
-        self.d_t = [torch.empty_like(self.h_t, device=dev) for _ in range(2)]
+        self.d_qt = [torch.empty_like(self.h_qt, device=dev) for _ in range(2)]
+        self.d_q = [self.d_qt[i][:nq] for i in range(2)]
+        self.d_t = [self.d_qt[i][nq:] for i in range(2)]
         # per slot: scores, target_begins, CIGAR lengths (written there by the plan) + the CIGAR byte total
         self.d_rec = [torch.zeros(3 * P + 1, dtype=torch.int32, device=dev) for _ in range(2)]
         self.plans = [DevicePlan(aligner, batch, type, match, mismatch, gap, want_cigar,
@@ -611,15 +627,23 @@ class HostPipeline:
         self.h_cig = [torch.empty(cap, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
         E = lambda: [torch.cuda.Event() for _ in range(2)]  # noqa: E731
         self.ev_in, self.ev_done, self.ev_rec, self.ev_cig = E(), E(), E(), E()
+        # per slot: the compacted CIGAR bytes and offsets, allocated once
+        self.cbuf = [self.plans[i].compact_buffers() for i in range(2)] if self.want_cigar else [None, None]
         self.used = [False, False]  # slot has a step in flight (its downloads may still run)
         self.prev = None            # (slot, device CIGAR bytes) of the previous step
         self.last = None
         self.k = 0
 
-    def _download_cigars(self, i, dst):
+    def _download(self, i, dst):
+        """Slot i's step, once its kernels are done: the records, then exactly
+        its CIGAR bytes (posted only now that their data is ready)."""
         torch = self.torch
+        self.ev_done[i].synchronize()  # the step's kernels are done
+        with torch.cuda.stream(self.down):
+            self.h_rec[i].copy_(self.d_rec[i], non_blocking=True)
+            self.ev_rec[i].record(self.down)
         if self.want_cigar:
-            self.ev_rec[i].synchronize()  # step's records are in (its kernels are done)
+            self.ev_rec[i].synchronize()
             nbytes = int(self.h_rec[i][3 * self.P])
             with torch.cuda.stream(self.down):
                 if nbytes:
@@ -633,38 +657,31 @@ class HostPipeline:
         torch, P = self.torch, self.P
         i = self.k % 2
         self.k += 1
-        if self.used[i]:
-            self.ev_cig[i].synchronize()  # slot i's host buffers of two steps ago are filled
+        # inputs of this step: the kernels of two steps ago (slot i) are done (the
+        # host saw them finish during the previous step)
         with torch.cuda.stream(self.up):
-            self.up.wait_event(self.ev_done[i])  # kernels of two steps ago no longer read these inputs
-            self.d_q[i].copy_(self.h_q, non_blocking=True)
-            self.d_t[i].copy_(self.h_t, non_blocking=True)
+            self.d_qt[i].copy_(self.h_qt, non_blocking=True)
             self.ev_in[i].record(self.up)
         plan = self.plans[i]
         with torch.cuda.stream(self.compute):
             self.compute.wait_event(self.ev_in[i])
-            self.compute.wait_event(self.ev_rec[i])  # (the slot's records of two steps ago are down)
+            if self.used[i]:  # the slot's results of two steps ago are down (a wait on the device)
+                self.compute.wait_event(self.ev_cig[i])
             plan.run()
             rec = self.d_rec[i]
             dst = None
             if self.want_cigar:
-                dst, off = plan.compact_cigars()
+                dst, off = plan.compact_cigars(out=self.cbuf[i])
                 rec[3 * P:].copy_(off[-1:], non_blocking=True)
             self.ev_done[i].record(self.compute)
-        if dst is not None:
-            dst.record_stream(self.down)
         self.used[i] = True
-        if self.prev is not None:  # the previous step's CIGAR bytes, ahead of this step's records
-            self._download_cigars(*self.prev)
-        with torch.cuda.stream(self.down):
-            self.down.wait_event(self.ev_done[i])
-            self.h_rec[i].copy_(rec, non_blocking=True)
-            self.ev_rec[i].record(self.down)
+        if self.prev is not None:  # the previous step's results (its kernels end as this step's begin)
+            self._download(*self.prev)
         self.prev = (i, dst)
 
     def drain(self):
         if self.prev is not None:
-            self._download_cigars(*self.prev)
+            self._download(*self.prev)
             self.prev = None
         self.torch.cuda.synchronize(self.dev)
 

@@ -190,6 +190,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
             a1.begin = ch.sbegin;
             a1.count = ch.scount;
             if (ch.dcount || ch.fcount) {  // beside the packed fill: fork onto the aux stream, join below
+                if (int r = ta_host::lazy_stream(ctx, ctx->aux)) return r;
                 TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
                 TA_HIP(ctx, hipStreamWaitEvent(ctx->aux, ctx->ev_fork, 0));
                 TA_HIP(ctx, ta::launch_fill(h.type, h.want_cigar, h.wide, a1, ctx->aux));
@@ -217,6 +218,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
                     TA_HIP(ctx, hipMemsetAsync(d.ticket, 0, 4, s));
                 }
                 if (ch.fcount) {  // beside the flexible fill: fork onto aux2 (after the counter reset), join below
+                    if (int r = ta_host::lazy_stream(ctx, ctx->aux2)) return r;
                     TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
                     TA_HIP(ctx, hipStreamWaitEvent(ctx->aux2, ctx->ev_fork, 0));
                     TA_HIP(ctx, ta::launch_dual(h.type, h.want_cigar, d, ctx->aux2));
@@ -359,10 +361,8 @@ int ta_context_create(int device, ta_context** out) {
     auto* c = new ta_context();
     c->device = device;
     c->cu_count = (uint32_t)std::max(1, prop.multiProcessorCount);
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->aux2, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
+    // (streams: created on first use, ta_host::lazy_stream)
+    if (hipSetDevice(device) != hipSuccess || hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_last, hipEventDisableTiming) != hipSuccess) {

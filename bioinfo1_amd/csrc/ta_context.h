@@ -53,6 +53,20 @@ inline int fail(ta_context* ctx, int code, const std::string& msg) {
     return code;
 }
 
+// A context's own streams are created on first use: each HIP stream takes one
+// of the process's few hardware queues (GPU_MAX_HW_QUEUES, 4 by default), and
+// streams beyond that share queues, where a copy queued behind another
+// stream's kernel waits for it.  A caller that drives plans on its own
+// streams (config 2: the whole batch in one dual fill) then creates none.
+inline int lazy_stream(ta_context* ctx, hipStream_t& s) {
+    if (s) return TA_OK;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        s = nullptr;
+        return fail(ctx, TA_ERR_DEVICE, "hipStreamCreateWithFlags failed");
+    }
+    return TA_OK;
+}
+
 #define TA_HIP(ctx, expr)                                                                                    \
     do {                                                                                                     \
         hipError_t e_ = (expr);                                                                              \

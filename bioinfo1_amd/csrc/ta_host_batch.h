@@ -96,6 +96,7 @@ inline int host_batch(ta_context* ctx, HostPlan& hp, uint32_t n_pairs, const cha
                       char* arena, uint64_t arena_bytes, uint64_t* cigar_off, uint32_t* cigar_len) {
     (void)qlen;
     (void)tlen;
+    if (int r = lazy_stream(ctx, ctx->stream)) return r;
     hipStream_t s = ctx->stream;
     const uint64_t P = n_pairs;
     // ---- inputs: plan arrays + offsets (+ small sequences) in one pinned block

@@ -14,7 +14,7 @@ hp = HostPipeline(al, b, 1, 1, -1, -1, True)
 for _ in range(3):
     hp.step()
 hp.drain()
-orig = hp._download_cigars
+orig = hp._download
 waits = []
 
 
@@ -24,7 +24,7 @@ def timed(i, dst):
     waits.append(time.perf_counter() - t0)
 
 
-hp._download_cigars = timed
+hp._download = timed
 t0 = time.perf_counter()
 steps = []
 for _ in range(10):
