@@ -294,9 +294,11 @@ int ta_server_align(ta_server* s, const char* q, uint32_t n, const char* t, uint
     s->active.fetch_add(1);
     s->last_call.store(now_ns());
     {
+        // (no hipEventQuery on this path: a HIP call per request costs microseconds;
+        // a kernel that ended under a running server -- its heartbeat timed out --
+        // is noticed by the wait below within 10 ms and restarted)
         std::lock_guard<std::mutex> lk(s->mu);
-        if (!s->running || s->ended()) {
-            s->running = false;
+        if (!s->running) {
             if (int r = s->start_locked()) {
                 s->active.fetch_sub(1);
                 s->busy[k].store(0);
