@@ -409,110 +409,154 @@ __device__ __forceinline__ uint32_t sys_load(const uint32_t* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// ---- small pairs (n <= 64, m <= 1024): one query row per lane, all in LDS.
+// ---- small pairs: R = 1, 2 or 4 query rows per lane (n <= 64R), all in LDS.
 // The batch fill gives a lane 16 rows; for one lone pair that makes every step
 // a 16-row dependent chain on an otherwise idle CU (a 5x9 pair: ~11 us of fill
-// and walk, 200x200 ~170 us).  Here lane l owns row l + 1 and steps along the
-// anti-diagonals (lane l at column t - l + 1 at step t; up and diag arrive
-// from lane l - 1 by DPP wave_shr:1 as in the batch fill), with the
-// reference's int32 cell rule verbatim (team_alignment.cpp:102-116 / :172-194 /
-// :250-263: strict '>' in the order MATCH, INSERT, DELETE; '-' free gaps; the
-// local clamp and first strict row-major maximum; the semi-global column-m
-// then row-n goal).  Codes: 2 bits per cell (M 0, I 1, D 2, local cost 0 =
-// STOP 3), 16 steps per dword, [step / 16][lane] in LDS.  The walk (:123-138,
-// :201-217, :286-315) runs on uniform values reading LDS, the RLE is formatted
-// lane-parallel (:145-160, "1\0" for an empty op string) and goes straight
-// into the host slot.
-constexpr uint32_t kSmallQ = 64, kSmallT = 1024;
-constexpr uint32_t kSmallCodeDw = (kSmallT + kSmallQ - 1 + 15) / 16 * kWave;
+// and walk, 200x200 ~170 us).  Here lane l owns rows lR + 1 .. lR + R and steps
+// along the anti-diagonals (lane l at column t - l + 1 at step t; up and diag
+// of its first row arrive from lane l - 1's last row by DPP wave_shr:1 as in
+// the batch fill), with the reference's int32 cell rule verbatim
+// (team_alignment.cpp:102-116 / :172-194 / :250-263: strict '>' in the order
+// MATCH, INSERT, DELETE; '-' free gaps; the local clamp and first strict
+// row-major maximum; the semi-global column-m then row-n goal).  Codes: 2 bits
+// per cell (M 0, I 1, D 2, local cost 0 = STOP 3), 16 / R steps per dword,
+// [step / (16 / R)][lane] in LDS.  The walk (:123-138, :201-217, :286-315) runs
+// on uniform values reading LDS, the RLE is formatted lane-parallel (:145-160,
+// "1\0" for an empty op string) and goes straight into the host slot.
+constexpr uint32_t kSmallQ = 256, kSmallT = 1024;
+constexpr uint32_t kSmallCodeDw = 68 * kWave;  // (steps x R) / 16 dwords per lane <= 68
 struct SmallLds {
     uint32_t codes[kSmallCodeDw];
-    uint32_t runs[kSmallQ + kSmallT + 4];
+    uint32_t runs[kSmallT + 64 + 4];  // at most n + m runs (n + m <= 1,088 for every admitted shape)
     uint8_t q[kSmallQ];
     uint8_t t[kSmallT];
-    char text[2 * (kSmallQ + kSmallT) + 16];
+    char text[2 * (kSmallT + 64) + 16];
 };
+// Rows per lane for an n x m pair (0: not a small pair): the fewest with
+// n <= 64R whose codes fit (m + ceil(n / R) - 1) * R <= 1,088.
+__device__ __forceinline__ uint32_t small_rows(uint32_t n, uint32_t m) {
+    if (n == 0 || m == 0 || m > kSmallT) return 0;
+    for (uint32_t R = 1; R <= 4; R <<= 1)
+        if (n <= 64u * R && (m + (n + R - 1) / R - 1) * R <= 16u * 68u) return R;
+    return 0;
+}
 
-template <int MODE>
+template <int MODE, int R>
 __device__ __forceinline__ PairOut serve_small(const FillArgs& a, uint32_t n, uint32_t m, bool want, SmallLds& L,
                                                char* out_text, int lane) {
+    constexpr uint32_t SPD = 16 / R;  // steps per code dword
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const int init = (MODE == kGlobal) ? gap : 0;  // :62-74
     const uint32_t l = (uint32_t)lane;
-    const bool row = l < n;
-    const uint32_t qb = L.q[min(l, n - 1u)];
-    const int upg = (qb == (uint32_t)'-') ? 0 : gap;  // indel(query[i-1]), :25-28
-    int H = wmul(l + 1u, init);                      // H(i, 0), :83-86; kept while the lane is idle
-    int recv = 0;                                    // lane 0's first diag is H(0, 0) = 0
+    const uint32_t nl = (n + R - 1) / R;  // lanes in use
+    uint32_t qb[R];
+    int upg[R], H[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t i0 = l * R + r;  // row i0 + 1
+        qb[r] = L.q[min(i0, n - 1u)];
+        upg[r] = (qb[r] == (uint32_t)'-') ? 0 : gap;  // indel(query[i-1]), :25-28
+        H[r] = wmul(i0 + 1u, init);                    // H(i, 0), :83-86; kept while the lane is idle
+    }
+    int recv = 0;  // lane 0's first diag is H(0, 0) = 0
+    // local: the lane's best cell (row-major first: larger h, then smaller row, then smaller j)
     int bh = INT_MIN, rb = INT_MIN;
-    uint32_t bj = 0, rbj = 0, acc = 0;
-    const uint32_t steps = m + n - 1u;
+    uint32_t br = 0, bj = 0, rbj = 0, acc = 0;
+    const uint32_t rn = (n - 1u) % R;  // row n's register in lane (n - 1) / R
+    const uint32_t steps = m + nl - 1u;
     uint32_t tnext = L.t[min(0u - l, m - 1u) & 0x3FFu];
     for (uint32_t t = 0; t < steps; ++t) {
-        const int dg = recv;                          // H(i-1, j-1)
-        recv = wave_shr1(wmul(t + 1u, init), H);      // H(i-1, j); lane 0: row 0, :89-92
+        int dg = recv;                                // H(row above, j - 1)
+        recv = wave_shr1(wmul(t + 1u, init), H[R - 1]);  // H(row above, j); lane 0: row 0, :89-92
         const uint32_t tb = tnext;
         tnext = L.t[min(t + 1u - l, m - 1u) & 0x3FFu];  // next column's target byte (clamped, unused when idle)
         const int j = (int)t - lane + 1;
-        uint32_t c = 0;
-        if (row && j >= 1 && j <= (int)m) {
-            const int diag = wadd(dg, qb == tb ? ma : mi);  // match_func, :20-23
-            const int left = wadd(H, tb == (uint32_t)'-' ? 0 : gap);
-            const int up = wadd(recv, upg);
-            int h = diag;
-            if (left > h) {
-                h = left;
-                c = 1;
-            }
-            if (up > h) {
-                h = up;
-                c = 2;
-            }
-            if (MODE == kLocal) {
-                if (h < 0) h = 0;  // :185
-                if (h == 0) c = 3;  // the walk stops here (:202)
-                if (h > bh) {       // :186, the first column keeps a tie
-                    bh = h;
-                    bj = (uint32_t)j;
+        uint32_t c4 = 0;
+        if (l < nl && j >= 1 && j <= (int)m) {
+            int up_in = recv;
+            const int lg = tb == (uint32_t)'-' ? 0 : gap;
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const uint32_t i0 = l * R + r;
+                const int old = H[r];
+                if (i0 < n) {
+                    const int diag = wadd(dg, qb[r] == tb ? ma : mi);  // match_func, :20-23
+                    const int left = wadd(old, lg);
+                    const int up = wadd(up_in, upg[r]);
+                    int h = diag;
+                    uint32_t c = 0;
+                    if (left > h) {
+                        h = left;
+                        c = 1;
+                    }
+                    if (up > h) {
+                        h = up;
+                        c = 2;
+                    }
+                    if (MODE == kLocal) {
+                        if (h < 0) h = 0;  // :185
+                        if (h == 0) c = 3;  // the walk stops here (:202)
+                        if (h > bh || (h == bh && (uint32_t)r < br)) {  // :186 in row-major order
+                            bh = h;
+                            br = r;
+                            bj = (uint32_t)j;
+                        }
+                    }
+                    if (MODE == kSemi && i0 == n - 1u && h > rb) {  // row n, :272-278
+                        rb = h;
+                        rbj = (uint32_t)j;
+                    }
+                    H[r] = h;
+                    c4 |= c << (2u * r);
                 }
+                dg = old;  // the next row's diag: this row's value one column left
+                up_in = H[r];
             }
-            if (MODE == kSemi && l == n - 1u && h > rb) {  // row n, :272-278
-                rb = h;
-                rbj = (uint32_t)j;
-            }
-            H = h;
         }
-        acc |= c << (2u * (t & 15u));
-        if ((t & 15u) == 15u || t + 1u == steps) {
-            L.codes[(t >> 4) * kWave + l] = acc;
+        acc |= c4 << (2u * R * (t % SPD));
+        if (t % SPD == SPD - 1u || t + 1u == steps) {
+            L.codes[(t / SPD) * kWave + l] = acc;
             acc = 0;
         }
     }
     PairOut o{0, 0, n, m, 0, 0};
     if (MODE == kGlobal) {
-        o.score = rdlane(H, n - 1u);  // H(n, m)
+        int hn = H[0];
+#pragma unroll
+        for (int r = 1; r < R; ++r) hn = ((uint32_t)r == rn) ? H[r] : hn;
+        o.score = rdlane(hn, (n - 1u) / R);  // H(n, m)
     } else if (MODE == kLocal) {
-        const int mx = wave_max(row ? bh : INT_MIN);
-        const int fl = first_lane(row && bh == mx);
+        // best h, then the smallest row: lanes hold ascending rows
+        const int mx = wave_max(l < nl ? bh : INT_MIN);
+        const int fl = first_lane(l < nl && bh == mx);
         o.score = mx;
-        o.gi = (uint32_t)fl + 1u;
+        o.gi = (uint32_t)fl * R + (uint32_t)rdlane((int)br, (uint32_t)fl) + 1u;
         o.gj = (uint32_t)rdlane((int)bj, (uint32_t)fl);
         o.tb = o.gj + 1u;  // :197-199
     } else {
         // column m from row 0 (cost 0), strict '>' (:265-271), then row n (:272-278)
-        const int mx = wave_max(row ? H : INT_MIN);
+        int cv = INT_MIN;
+        uint32_t cr = 0;
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+            if (l * R + r < n && H[r] > cv) {
+                cv = H[r];
+                cr = r;
+            }
+        const int mx = wave_max(cv);
         int best = 0;
         o.gi = 0;
         o.gj = m;
         if (mx > best) {
             best = mx;
-            o.gi = (uint32_t)first_lane(row && H == mx) + 1u;
+            const int fl = first_lane(cv == mx);
+            o.gi = (uint32_t)fl * R + (uint32_t)rdlane((int)cr, (uint32_t)fl) + 1u;
         }
-        const int r = rdlane(rb, n - 1u);
-        if (r > best) {
-            best = r;
+        const int rbv = rdlane(rb, (n - 1u) / R);
+        if (rbv > best) {
+            best = rbv;
             o.gi = n;
-            o.gj = (uint32_t)rdlane((int)rbj, n - 1u);
+            o.gj = (uint32_t)rdlane((int)rbj, (n - 1u) / R);
         }
         o.score = best;
     }
@@ -535,8 +579,8 @@ __device__ __forceinline__ PairOut serve_small(const FillArgs& a, uint32_t n, ui
         else if (jj == m) push(2u, n - i);
     }
     auto code_at = [&](uint32_t ci, uint32_t cj) {
-        const uint32_t st = cj + ci - 2u;
-        return (L.codes[(st >> 4) * kWave + (ci - 1u)] >> (2u * (st & 15u))) & 3u;
+        const uint32_t ln = (ci - 1u) / R, r = (ci - 1u) % R, st = cj + ln - 1u;
+        return (L.codes[(st / SPD) * kWave + ln] >> (2u * (R * (st % SPD) + r))) & 3u;
     };
     if (MODE == kLocal) {
         while (i >= 1u && jj >= 1u) {  // cost > 0 (boundary cells cost 0)
@@ -632,12 +676,14 @@ __device__ __forceinline__ void serve_one(const ServeArgs& sa, uint32_t s, char*
     char* cslot = a.slots + (uint64_t)s * ((cigar_slot_bytes(kSrvQMax, kSrvTMax) + 255) & ~255ull);
     if (n > kSrvQMax || m > kSrvTMax) {
         status = TA_ERR_ARG;  // (the host never posts such a pair)
-    } else if (n >= 1 && m >= 1 && n <= kSmallQ && m <= kSmallT) {
-        if (lane >= 6 && lane < 10) *reinterpret_cast<uint4*>(L.q + 16u * (uint32_t)(lane - 6)) = qv;
+    } else if (const uint32_t R = small_rows(n, m)) {
+        if (lane >= 6 && lane < 6 + (int)(kSmallQ / 16)) *reinterpret_cast<uint4*>(L.q + 16u * (uint32_t)(lane - 6)) = qv;
         *reinterpret_cast<uint4*>(L.t + 16u * (uint32_t)lane) = tv;
         __syncthreads();
         t1 = wall_clock64();
-        o = serve_small<MODE>(a, n, m, want, L, slot + kSrvCOff, lane);
+        if (R == 1) o = serve_small<MODE, 1>(a, n, m, want, L, slot + kSrvCOff, lane);
+        else if (R == 2) o = serve_small<MODE, 2>(a, n, m, want, L, slot + kSrvCOff, lane);
+        else o = serve_small<MODE, 4>(a, n, m, want, L, slot + kSrvCOff, lane);
         t2 = wall_clock64();
     } else {
         if (lane >= 6) *reinterpret_cast<uint4*>(dq + 16u * (uint32_t)(lane - 6)) = qv;

@@ -697,9 +697,9 @@ def test_single_pair_server(kat_cases, random_cases, oracle):
 
 
 def test_single_pair_server_small(oracle):
-    """The server's small-pair path (n <= 64 query rows, m <= 1,024: one row per
-    lane, codes in LDS, serve_small): random pairs at its edges (n = 1 / 64,
-    m = 1 / 1,024, ragged in between) over A C G T - N, several scoring schemes
+    """The server's small-pair path (one, two or four query rows per lane up to
+    n = 256, codes in LDS, serve_small): random pairs at its edges (n = 1 / 64 /
+    128 / 256, m up to 1,024 / 481 / 209, ragged in between) over A C G T - N, several scoring schemes
     (positive gaps and matches below mismatches included), every mode, CIGAR
     and score-only, against the oracle."""
     from bioinfo1_amd import synth as S
@@ -708,6 +708,10 @@ def test_single_pair_server_small(oracle):
     rng = np.random.default_rng(0x5A11)
     shapes = [(1, 1), (1, 1024), (64, 1), (64, 1024), (64, 64), (2, 3), (63, 1023), (17, 200)]
     shapes += [(int(rng.integers(1, 65)), int(rng.integers(1, 1025))) for _ in range(40)]
+    # two and four rows per lane (n up to 128 / 256, m as the LDS code budget allows)
+    shapes += [(65, 480), (128, 481), (100, 300), (129, 200), (200, 200), (256, 209), (256, 1), (255, 33)]
+    shapes += [(int(rng.integers(65, 129)), int(rng.integers(1, 482))) for _ in range(12)]
+    shapes += [(int(rng.integers(129, 257)), int(rng.integers(1, 210))) for _ in range(12)]
     pairs = []
     for k, (n, m) in enumerate(shapes):
         a = b"ACGT-N" if k % 3 == 0 else b"ACGT"
