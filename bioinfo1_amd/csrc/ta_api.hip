@@ -35,6 +35,9 @@ struct ta_plan {
     uint32_t *d_flex_task_off = nullptr, *d_tickets = nullptr, *d_err = nullptr, *d_flex_tasks = nullptr;
     void* d_pout = nullptr;  // PassOut[2] per flex task
     void* d_dpout = nullptr;  // PassOut[2] per (pass, dual couple) of one multi-pass chunk
+    uint32_t* d_stask_off = nullptr;  // pipelined int32 fill: per single, its first task
+    uint64_t* d_stasks = nullptr;     // ... its tasks in ticket order
+    void* d_spout = nullptr;          // ... PassOut per task
 };
 
 namespace {
@@ -45,8 +48,9 @@ bool valid_type(int t) { return t == TA_GLOBAL || t == TA_LOCAL || t == TA_SEMI_
 // `upload_end` is copied from the host (the error word and ticket counters
 // as zeros); goal cells, the hand-back list and the pass results are device-only.
 struct PlanOffs {
-    uint64_t qlen, tlen, order, singles, duals, flexes, task_off, tasks, ptr_off, bnd_off, slot_off, err, tickets;
-    uint64_t goal_i, goal_j, fb, pout, dpout;
+    uint64_t qlen, tlen, order, singles, duals, flexes, task_off, tasks, stask_off, stasks, ptr_off, bnd_off, slot_off,
+        err, tickets;
+    uint64_t goal_i, goal_j, fb, pout, dpout, spout;
 };
 
 // PassOut[2] (24 bytes each) per (pass, couple) of the largest multi-pass dual chunk
@@ -72,11 +76,13 @@ PlanOffs layout_uploaded(const ta::Plan& h, ta::BlockLayout& L) {
     o.flexes = L.add(vbytes(h.flexes));
     o.task_off = L.add(vbytes(h.flex_task_off));
     o.tasks = L.add(vbytes(h.flex_tasks));
+    o.stask_off = L.add(vbytes(h.single_task_off));
+    o.stasks = L.add(vbytes(h.single_tasks));
     o.ptr_off = L.add(vbytes(h.ptr_off));
     o.bnd_off = L.add(vbytes(h.bnd_off));
     o.slot_off = L.add(vbytes(h.slot_off));
     o.err = L.add(4);
-    o.tickets = L.add(8ull * h.chunks.size());  // per chunk: flex, then dual
+    o.tickets = L.add(12ull * h.chunks.size());  // per chunk: flex, then dual, then pipelined int32
     return o;
 }
 
@@ -86,6 +92,7 @@ void layout_scratch(const ta::Plan& h, ta::BlockLayout& L, PlanOffs& o) {
     o.fb = L.add(4ull * (h.n_dual_pairs + h.chunks.size()));
     o.pout = L.add(h.flexes.empty() ? 0 : h.flex_task_off.back() * 48ull + 16);
     o.dpout = L.add(dual_pout_bytes(h));
+    o.spout = L.add(h.single_tasks.size() * 24ull);
 }
 
 void pack(const ta::Plan& h, const PlanOffs& o, uint8_t* base) {
@@ -100,11 +107,13 @@ void pack(const ta::Plan& h, const PlanOffs& o, uint8_t* base) {
     put(o.flexes, h.flexes);
     put(o.task_off, h.flex_task_off);
     put(o.tasks, h.flex_tasks);
+    put(o.stask_off, h.single_task_off);
+    put(o.stasks, h.single_tasks);
     put(o.ptr_off, h.ptr_off);
     put(o.bnd_off, h.bnd_off);
     put(o.slot_off, h.slot_off);
     std::memset(base + o.err, 0, 4);
-    std::memset(base + o.tickets, 0, 8ull * h.chunks.size());
+    std::memset(base + o.tickets, 0, 12ull * h.chunks.size());
 }
 
 void bind(ta_plan* pl, uint8_t* d, const PlanOffs& o) {
@@ -128,6 +137,9 @@ void bind(ta_plan* pl, uint8_t* d, const PlanOffs& o) {
     pl->d_fb = u32(o.fb);
     pl->d_pout = d + o.pout;
     pl->d_dpout = d + o.dpout;
+    pl->d_stask_off = u32(o.stask_off);
+    pl->d_stasks = u64(o.stasks);
+    pl->d_spout = d + o.spout;
 }
 
 int check_args(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type) {
@@ -157,7 +169,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         // memory left there (traceback codes of a freed workspace, other
         // plans' records) must not survive: zero it (tag 0 is never valid)
         // before any kernel of this chunk is enqueued.
-        if ((ch.fcount || ch.dpasses > 1) && ch.bnd_words) TA_HIP(ctx, hipMemsetAsync(d_bnd, 0, ch.bnd_words * 4ull, s));
+        if ((ch.fcount || ch.dpasses > 1 || ch.spasses > 1) && ch.bnd_words) TA_HIP(ctx, hipMemsetAsync(d_bnd, 0, ch.bnd_words * 4ull, s));
         ta::FillArgs a{};
         a.order = pl->d_order;
         a.begin = ch.begin;
@@ -189,6 +201,15 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
             a1.order = pl->d_singles;
             a1.begin = ch.sbegin;
             a1.count = ch.scount;
+            if (ch.spasses > 1) {  // one wave per (pair, pass), tickets pass-major
+                a1.task_off = pl->d_stask_off;
+                a1.tasks64 = pl->d_stasks;
+                a1.ticket = pl->d_tickets + 2 * h.chunks.size() + c;
+                a1.n_tasks = h.single_task_off[ch.sbegin + ch.scount] - h.single_task_off[ch.sbegin];
+                a1.err = pl->d_err;
+                a1.pout = pl->d_spout;
+                TA_HIP(ctx, hipMemsetAsync(a1.ticket, 0, 4, s));
+            }
             if (ch.dcount || ch.fcount) {  // beside the packed fill: fork onto the aux stream, join below
                 if (int r = ta_host::lazy_stream(ctx, ctx->aux)) return r;
                 TA_HIP(ctx, hipEventRecord(ctx->ev_fork, s));
@@ -322,7 +343,9 @@ struct LinearHostPlan final : ta_host::HostPlan {
     void bind(uint8_t* dev) override { ::bind(pl, dev, o); }
     int execute(const ta_device_io* io, hipStream_t s) override { return exec(pl, io, s, UINT32_MAX, true, true); }
     uint64_t slots_bytes() const override { return pl->h.slots_bytes; }
-    uint64_t err_offset() const override { return pl->h.flexes.empty() && pl->h.duals.empty() ? UINT64_MAX : o.err; }
+    uint64_t err_offset() const override {
+        return pl->h.flexes.empty() && pl->h.duals.empty() && pl->h.single_tasks.empty() ? UINT64_MAX : o.err;
+    }
     const char* err_message() const override {
         return "packed fill: a pass hand-off poll timed out; results of this batch are invalid";
     }
@@ -488,13 +511,13 @@ int ta_plan_execute_traceback(ta_plan* pl, const ta_device_io* io, void* stream,
 
 int ta_plan_check(ta_plan* pl) {
     if (!pl) return TA_ERR_ARG;
-    if (pl->h.flexes.empty() && pl->h.duals.empty()) return TA_OK;
+    if (pl->h.flexes.empty() && pl->h.duals.empty() && pl->h.single_tasks.empty()) return TA_OK;
     uint32_t err = 0;
     TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
     TA_HIP(pl->ctx, hipMemcpy(&err, pl->d_err, 4, hipMemcpyDeviceToHost));
     if (!err) return TA_OK;
     TA_HIP(pl->ctx, hipMemset(pl->d_err, 0, 4));
-    return fail(pl->ctx, TA_ERR_DEVICE, "packed fill: a pass hand-off poll timed out; results of this plan are invalid");
+    return fail(pl->ctx, TA_ERR_DEVICE, "fill: a pass hand-off poll timed out; results of this plan are invalid");
 }
 
 int ta_compact_cigars(ta_context* ctx, uint32_t n_pairs, const char* cigar_slots, const uint64_t* cigar_start,

@@ -58,6 +58,9 @@ struct FillArgs {
     uint32_t epoch;            // tag base of this launch's pass hand-off records
     uint32_t* err;             // a poll gave up (never on a correct schedule)
     void* pout;                // PassOut[2] per task (plan-global task index)
+    // pipelined int32 fill (fill_pipe_kernel; task_off = per single, ticket,
+    // n_tasks, err, pout = PassOut per task as above): ticket order, single << 32 | pass
+    const uint64_t* tasks64;
 };
 
 struct TraceArgs {

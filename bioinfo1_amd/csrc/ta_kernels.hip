@@ -61,6 +61,46 @@ __device__ __forceinline__ PairOut degenerate(int gap, uint32_t n, uint32_t m) {
     return o;
 }
 
+// The pass boundary row.  A wave that sweeps all of a pair's passes itself
+// keeps it in place (B: one int32 per column, rewritten by every pass).  In
+// the pipelined fill (one wave per (pair, pass), fill_pipe_kernel) pass p's
+// bottom row goes to 8-byte records tag << 32 | H in the pair's region, two
+// buffers by pass parity, written with relaxed agent-scope stores; pass p + 1
+// polls 64 columns at a time until every record carries the tag it expects
+// (the data is its own flag, as ta_flex.hip / ta_dual.hip).
+struct BndIo {
+    int32_t* B;
+    uint64_t* rec_w;        // null: B (or the last pass)
+    const uint64_t* rec_r;  // null: B (or pass 0)
+    uint32_t tag_w, tag_r;
+    uint32_t* err;
+};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64k;
+
+// columns 64k + lane + 1 of the previous pass's bottom row
+__device__ __forceinline__ int load_bnd(const BndIo& io, uint32_t m, uint32_t k, int lane) {
+    if (!io.rec_r) return load_bchunk(io.B, m, k, lane);
+    const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+    const gu64k* r = (const gu64k*)(io.rec_r + j);
+    int v = 0;
+    for (uint32_t spins = 0;; ++spins) {
+        bool ok = true;
+        if (j <= m) {
+            const uint64_t x = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(x >> 32) == io.tag_r;
+            v = (int)(uint32_t)x;
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spins > (1u << 22)) {  // bounded: the kernel always ends
+            if (lane == 0) atomicOr(io.err, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return v;
+}
+
 // One pass = rows row_base+1 .. row_base+nrows of the query against the whole
 // target.  Compile-time specialisation:
 //   NV     valid rows of the last lane in use (every register index static);
@@ -74,7 +114,7 @@ __device__ __forceinline__ PairOut degenerate(int gap, uint32_t n, uint32_t m) {
 template <int MODE, bool CIGAR, bool WIDE, int NV, bool QDASH>
 __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
                                             uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
-                                            int32_t* B, int lane) {
+                                            const BndIo& B, int lane) {
     constexpr int R = kRows;
     constexpr bool SCALED = (MODE == kLocal) && !WIDE;
     constexpr int SC = SCALED ? 32 : 1;
@@ -123,8 +163,8 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
     uint32_t tcur = load_tchunk(T, m, 0, lane), tnext = load_tchunk(T, m, 1, lane);
     int bcur = 0, bnext = 0;
     if (pass > 0) {
-        bcur = load_bchunk(B, m, 0, lane);
-        bnext = load_bchunk(B, m, 1, lane);
+        bcur = load_bnd(B, m, 0, lane);
+        bnext = load_bnd(B, m, 1, lane);
     }
     const uint32_t steps = m + nl - 1;
     uint32_t* prow = CIGAR ? ptrs + (uint64_t)pass * Tmax * kWave : nullptr;
@@ -146,7 +186,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
         } else {
             if ((t & 63u) == 0 && t) {
                 bcur = bnext;
-                bnext = load_bchunk(B, m, (t >> 6) + 1, lane);
+                bnext = load_bnd(B, m, (t >> 6) + 1, lane);
             }
             top = rdlane(bcur, t & 63u);
         }
@@ -231,7 +271,13 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
                     rowbest_j = (uint32_t)j;
                 }
             }
-            if (has_next && (uint32_t)lane == nl - 1) B[j] = H[R - 1];
+            if (has_next && (uint32_t)lane == nl - 1) {
+                if (B.rec_w)
+                    __hip_atomic_store((gu64k*)(B.rec_w + j), ((uint64_t)B.tag_w << 32) | (uint32_t)H[R - 1],
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                else
+                    B.B[j] = H[R - 1];
+            }
         }
         if (CIGAR) prow[t * kWave + lane] = (accD << kDPlane) | accI;
     };
@@ -286,7 +332,7 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
 template <int MODE, bool CIGAR, bool WIDE, bool QDASH>
 __device__ __forceinline__ PassOut run_pass_nv(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
                                                uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
-                                               int32_t* B, int lane) {
+                                               const BndIo& B, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
     // Global needs NV only for the corner cell (read with a runtime select);
@@ -307,7 +353,7 @@ __device__ __forceinline__ PassOut run_pass_nv(const FillArgs& a, const uint8_t*
 template <int MODE, bool CIGAR, bool WIDE>
 __device__ __forceinline__ PassOut run_pass_any(const FillArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
                                                 uint32_t m, uint32_t pass, bool last_pass, uint32_t* ptrs,
-                                                int32_t* B, int lane) {
+                                                const BndIo& B, int lane) {
     // does any query row of this pass hold '-' (free vertical gap)?
     bool dash = false;
     const uint32_t row0 = pass * kPassRows + (uint32_t)lane * kRows;
@@ -324,7 +370,7 @@ __device__ __forceinline__ PassOut run_pass_any(const FillArgs& a, const uint8_t
 // the sequences; ptrs: the pair's code workspace; B: its pass boundary row.
 template <int MODE, bool CIGAR, bool WIDE>
 __device__ __forceinline__ PairOut fill_one(const FillArgs& a, uint32_t n, uint32_t m, const uint8_t* Q,
-                                            const uint8_t* T, uint32_t* ptrs, int32_t* B, char* slot, bool walk,
+                                            const uint8_t* T, uint32_t* ptrs, int32_t* Bw, char* slot, bool walk,
                                             int lane) {
     const WalkSeq seq0{Q, T, 0, a.match, a.mismatch, a.gap};
     if (n == 0 || m == 0) {
@@ -338,6 +384,7 @@ __device__ __forceinline__ PairOut fill_one(const FillArgs& a, uint32_t n, uint3
         return o;
     }
     const uint32_t passes = n_passes(n);
+    const BndIo B{Bw, nullptr, nullptr, 0, 0, nullptr};
     // running goal over passes (wave-uniform); semi starts from (0,m), cost 0
     int best_h = (MODE == kSemi) ? 0 : INT_MIN;
     uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
@@ -399,6 +446,74 @@ __global__ __launch_bounds__(kBlock) void fill_kernel(FillArgs a) {
     const uint32_t widx = wave_id();
     if (widx >= (a.count_dev ? *a.count_dev : a.count)) return;  // wave-uniform
     fill_pair<MODE, CIGAR, WIDE>(a, a.order ? a.order[a.begin + widx] : a.begin + widx, lane);
+}
+
+// The pipelined int32 fill: one wave per (pair, pass) of a chunk's singles
+// (order = the plan's singles).  A wave takes the next ticket; the tasks are
+// pass-major (every pair's pass 0, then every pass 1, ...; the planner's
+// single_tasks), so pass p - 1 of its pair belongs to a wave that took an
+// earlier ticket and is running: every poll ends.  The walk runs in the
+// traceback kernel after fill_combine_kernel has folded the passes.
+template <int MODE, bool CIGAR, bool WIDE>
+__global__ __launch_bounds__(kBlock) void fill_pipe_kernel(FillArgs a) {
+    const int lane = threadIdx.x & 63;
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(a.ticket, 1u);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+    if (tk >= a.n_tasks) return;
+    const uint64_t code = a.tasks64[a.task_off[a.begin] + tk];
+    const uint32_t w = (uint32_t)(code >> 32), pass = (uint32_t)code;
+    const uint32_t p = a.order[w];
+    const uint32_t n = a.qlen[p], m = a.tlen[p];  // both > 0: empty pairs have no task
+    const bool last_pass = pass + 1 == n_passes(n);
+    uint64_t* rec = reinterpret_cast<uint64_t*>(a.bnd + a.bnd_off[p]);  // 2 buffers x (m + 1) records
+    const uint64_t rb = (uint64_t)m + 1;
+    // tags: pass + 1 for pass p's row (never 0; the host zeroes the records before the launch)
+    const BndIo B{nullptr, last_pass ? nullptr : rec + (pass & 1u) * rb, pass ? rec + ((pass - 1u) & 1u) * rb : nullptr,
+                  pass + 1u, pass, a.err};
+    uint32_t* ptrs = CIGAR ? a.ptrs + a.ptr_off[p] : nullptr;
+    const PassOut o = run_pass_any<MODE, CIGAR, WIDE>(a, a.qbytes + a.qoff[p], a.tbytes + a.toff[p], n, m, pass,
+                                                      last_pass, ptrs, B, lane);
+    if (lane == 0) static_cast<PassOut*>(a.pout)[a.task_off[w] + pass] = o;
+}
+
+// After the pipelined fill: fold each pair's per-pass results in pass order
+// as fill_one does (the upper pass wins ties; semi: row n after column m).
+template <int MODE>
+__global__ void fill_combine_kernel(FillArgs a) {
+    const uint32_t w = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= a.begin + a.count) return;
+    const uint32_t p = a.order[w];
+    const uint32_t n = a.qlen[p], m = a.tlen[p];
+    PairOut r;
+    if (n == 0 || m == 0) {
+        r = degenerate<MODE>(a.gap, n, m);
+    } else {
+        const PassOut* po = static_cast<const PassOut*>(a.pout) + a.task_off[w];
+        const uint32_t passes = a.task_off[w + 1] - a.task_off[w];
+        int best_h = (MODE == kSemi) ? 0 : INT_MIN, corner = 0;
+        uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
+        for (uint32_t k = 0; k < passes; ++k) {
+            const PassOut& o = po[k];
+            if (MODE != kGlobal && o.h > best_h) {
+                best_h = o.h;
+                best_i = o.i;
+                best_j = o.j;
+            }
+            if (MODE == kSemi && k + 1 == passes && o.row_h > best_h) {
+                best_h = o.row_h;
+                best_i = n;
+                best_j = o.row_j;
+            }
+            if (MODE == kGlobal && k + 1 == passes) corner = o.corner;
+        }
+        r = PairOut{(MODE == kGlobal) ? corner : best_h, (MODE == kLocal) ? best_j + 1 : 0u,
+                    (MODE == kGlobal) ? n : best_i, (MODE == kGlobal) ? m : best_j, 0, 0};
+    }
+    a.score[p] = r.score;
+    a.target_begin[p] = r.tb;
+    a.goal_i[p] = r.gi;
+    a.goal_j[p] = r.gj;
 }
 
 #if TA_FILL_CIGAR
@@ -827,6 +942,15 @@ hipError_t launch_fill_mode<TA_FILL_MODE, (TA_FILL_CIGAR != 0)>(bool wide, const
     constexpr bool CIGAR = TA_FILL_CIGAR != 0;
     if (!a.count) return hipSuccess;
     const dim3 g = grid_for(a.count), b(kBlock);
+    if (a.tasks64) {  // one wave per (pair, pass), then the fold of the passes
+        if (a.n_tasks) {
+            const dim3 gt = grid_for(a.n_tasks);
+            if (MODE == kLocal && wide) hipLaunchKernelGGL((fill_pipe_kernel<MODE, CIGAR, MODE == kLocal>), gt, b, 0, s, a);
+            else hipLaunchKernelGGL((fill_pipe_kernel<MODE, CIGAR, false>), gt, b, 0, s, a);
+        }
+        hipLaunchKernelGGL(fill_combine_kernel<MODE>, dim3((a.count + 255) / 256), dim3(256), 0, s, a);
+        return hipGetLastError();
+    }
     // WIDE only changes the local argmax; other modes use one instantiation.
     if (MODE == kLocal && wide) hipLaunchKernelGGL((fill_kernel<MODE, CIGAR, MODE == kLocal>), g, b, 0, s, a);
     else hipLaunchKernelGGL((fill_kernel<MODE, CIGAR, false>), g, b, 0, s, a);

@@ -273,6 +273,10 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         for (uint32_t p : rest) units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
     }
     std::stable_sort(units.begin(), units.end(), [](const Unit& x, const Unit& y) { return x.cost > y.cost; });
+    // Multi-pass int32 pairs run one wave per (pair, pass) like the packed
+    // fills (their passes overlap instead of following each other on one
+    // wave); the walk then runs in the traceback kernel.
+    const bool pipe_singles = !(flags & kPlanSerialPasses);
     auto unit_codes = [&](size_t k) -> uint64_t {
         const Unit& u = units[k];
         if (!want_cigar) return 0;
@@ -280,7 +284,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     };
     auto unit_waves = [&](size_t k) -> uint64_t {
         const Unit& u = units[k];
-        return u.kind ? n_passes(qlen[u.a]) : 1;  // packed fills: one wave per (couple, pass)
+        // packed fills and pipelined int32 pairs: one wave per (pair or couple, pass)
+        return (u.kind || pipe_singles) && qlen[u.a] && tlen[u.a] ? n_passes(qlen[u.a]) : 1;
     };
     const std::vector<size_t> starts = chunk_starts(units.size(), budget_dw, wave_quantum, unit_codes, unit_waves);
     size_t next_cut = 1;
@@ -290,7 +295,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     auto open_chunk = [&]() {
         cur = Plan::Chunk{(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0,
                           (uint32_t)(pl.duals.size() / 2), 0, (uint32_t)(pl.flexes.size() / 2), 0,
-                          couples_before, 0, 0, 0};
+                          couples_before, 0, 0, 0, 0};
     };
     open_chunk();
     for (size_t k = 0; k < units.size(); ++k) {
@@ -315,6 +320,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
                 bw = std::max<uint64_t>(bw, 8ull * ((uint64_t)std::max(ma, mb) + 1));
             // dual: pair A holds the couple's packed hand-off records, 2 buffers x 8 bytes per column
             if (u.kind == 1 && h == 0 && n_passes(na) > 1) bw = std::max<uint64_t>(bw, 4ull * ((uint64_t)ma + 1));
+            // pipelined int32 fill: the pair's hand-off records, 2 buffers x 8 bytes per column
+            if (u.kind == 0 && pipe_singles && n_passes(na) > 1) bw = std::max<uint64_t>(bw, 4ull * ((uint64_t)ma + 1));
             bw += bw & 1;  // keep every region 8-byte aligned (64-bit hand-off records)
             cur.ptr_dwords += xd;
             cur.bnd_words += bw;
@@ -332,6 +339,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         } else {
             pl.singles.push_back(u.a);
             ++cur.scount;
+            if (pipe_singles && na && ma) cur.spasses = std::max(cur.spasses, n_passes(na));
         }
         if (u.kind) {
             pl.n_dual_pairs += 2;
@@ -342,7 +350,9 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     if (cur.count) pl.chunks.push_back(cur);
     // A fill kernel that walks its own pair only pays when nothing else of the
     // chunk runs in the separate traceback kernel anyway.
-    pl.fused = want_cigar && pl.n_dual_pairs == 0 && !(flags & kPlanUnfused);
+    bool piped = false;
+    for (const auto& c : pl.chunks) piped |= c.spasses > 1;
+    pl.fused = want_cigar && pl.n_dual_pairs == 0 && !(flags & kPlanUnfused) && !piped;
     // Local walks of short pairs: lane walks (one lane per pair steps cell by cell
     // through LDS tiles, ta_walk_lane.h; indel costs kept as int8).  Two pairs per
     // wave (32 lanes each, ta_walk2.h): 0.65 vs 0.77 ms for one pair per wave on
@@ -369,6 +379,20 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         for (uint32_t ps = 0; ps < maxp; ++ps)
             for (uint32_t w = ch.fbegin; w < ch.fbegin + ch.fcount; ++w)
                 if (pl.flex_task_off[w + 1] - pl.flex_task_off[w] > ps) pl.flex_tasks[at++] = w * 64u + ps;
+    }
+    if (piped) {
+        pl.single_task_off.assign(1, 0);
+        for (uint32_t p : pl.singles)
+            pl.single_task_off.push_back(pl.single_task_off.back() + (qlen[p] && tlen[p] ? n_passes(qlen[p]) : 0));
+        pl.single_tasks.assign(pl.single_task_off.back(), 0ull);
+        for (const auto& ch : pl.chunks) {
+            if (ch.spasses < 2) continue;  // single-pass singles: the one-wave-per-pair fill
+            uint32_t at = pl.single_task_off[ch.sbegin];
+            for (uint32_t ps = 0; ps < ch.spasses; ++ps)
+                for (uint32_t w = ch.sbegin; w < ch.sbegin + ch.scount; ++w)
+                    if (pl.single_task_off[w + 1] - pl.single_task_off[w] > ps)
+                        pl.single_tasks[at++] = ((uint64_t)w << 32) | ps;
+        }
     }
     for (const auto& c : pl.chunks) {
         pl.ws_ptr_dwords = std::max(pl.ws_ptr_dwords, c.ptr_dwords);

@@ -20,6 +20,7 @@ constexpr uint32_t kPlanNoFlex = 2u;     // no rebased (different-shape) couples
 constexpr uint32_t kPlanUnfused = 4u;    // int32-only plans: traceback as its own kernel
 constexpr uint32_t kPlanWalk1 = 8u;      // local walks: one pair per wave (traceback_pair)
 constexpr uint32_t kPlanWalk2 = 16u;     // local walks: two pairs per wave (ta_walk2.h), not lane walks
+constexpr uint32_t kPlanSerialPasses = 32u;  // int32 fill: one wave sweeps all of a pair's passes
 
 // Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
@@ -50,6 +51,12 @@ struct Plan {
     // per chunk, the chunk's flex tasks in ticket order (couple * 64 + pass),
     // pass-major: every couple's pass 0, then every pass 1, ...
     std::vector<uint32_t> flex_tasks;
+    // int32 fill of multi-pass singles, one wave per (pair, pass): per single
+    // (plan order), its first task (one per query pass; none for an empty
+    // pair); last entry = total.  Per chunk with spasses > 1, its tasks in
+    // ticket order (single << 32 | pass), pass-major.  Empty: no chunk is pipelined.
+    std::vector<uint32_t> single_task_off;
+    std::vector<uint64_t> single_tasks;
     std::vector<uint64_t> ptr_off, bnd_off, slot_off;
     struct Chunk {
         uint32_t begin, count;    // all pairs (traceback order)
@@ -59,6 +66,7 @@ struct Plan {
         uint32_t cbegin;          // couples (dual + flex) before this chunk: its slice of the hand-back list
         uint64_t ptr_dwords, bnd_words;
         uint32_t dpasses;         // largest pass count of the dual couples (> 1: one wave per couple and pass)
+        uint32_t spasses;         // largest pass count of the singles (> 1: one wave per pair and pass)
     };
     std::vector<Chunk> chunks;
     uint32_t n_dual_pairs = 0;  // pairs in packed couples (dual + flex)

@@ -9,6 +9,7 @@
 //                    random batches from T threads at once: every pair planned
 //                    exactly once, chunk / workspace / task invariants
 //   fastx PATH Q     the FASTA/FASTQ reader (tm_fastx.cpp): record count + checksum
+#include <algorithm>
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>
@@ -117,7 +118,10 @@ void check_linear(const ta::Plan& pl, uint64_t budget) {
     // units partition the pairs: singles + duals + flex (a self-coupled flex pair counts once)
     std::vector<int> unit(P, 0);
     for (uint32_t x : pl.singles) ++unit[x];
-    for (uint32_t x : pl.duals) ++unit[x];
+    for (size_t k = 0; k + 1 < pl.duals.size(); k += 2) {  // a lone pair may be coupled with itself
+        ++unit[pl.duals[k]];
+        if (pl.duals[k + 1] != pl.duals[k]) ++unit[pl.duals[k + 1]];
+    }
     for (size_t k = 0; k + 1 < pl.flexes.size(); k += 2) {
         ++unit[pl.flexes[k]];
         if (pl.flexes[k + 1] != pl.flexes[k]) ++unit[pl.flexes[k + 1]];
@@ -155,6 +159,38 @@ void check_linear(const ta::Plan& pl, uint64_t budget) {
             CHECK(ps >= prev_pass);
             prev_pass = ps;
             CHECK(ps < pl.flex_task_off[w + 1] - pl.flex_task_off[w]);
+        }
+    }
+    // pipelined int32 tasks: every (single, pass) of a chunk with spasses > 1
+    // exactly once, pass-major; its pair holds two record buffers
+    bool piped = false;
+    for (const auto& c : pl.chunks) piped |= c.spasses > 1;
+    CHECK(piped == !pl.single_task_off.empty());
+    if (piped) {
+        CHECK(pl.single_task_off.size() == pl.singles.size() + 1);
+        CHECK(!pl.fused);
+        for (const auto& c : pl.chunks) {
+            if (c.spasses < 2) continue;
+            std::set<uint64_t> seen_tasks;
+            uint32_t prev_pass = 0, maxp = 0;
+            for (uint32_t w = c.sbegin; w < c.sbegin + c.scount; ++w) {
+                const uint32_t x = pl.singles[w];
+                const uint32_t want = pl.qlen[x] && pl.tlen[x] ? ta::n_passes(pl.qlen[x]) : 0;
+                CHECK(pl.single_task_off[w + 1] - pl.single_task_off[w] == want);
+                maxp = std::max(maxp, want);
+                if (want > 1) CHECK(pl.bnd_off[x] + 4ull * (pl.tlen[x] + 1) <= c.bnd_words && pl.bnd_off[x] % 2 == 0);
+            }
+            CHECK(maxp == c.spasses);
+            for (uint32_t k = pl.single_task_off[c.sbegin]; k < pl.single_task_off[c.sbegin + c.scount]; ++k) {
+                const uint64_t code = pl.single_tasks[k];
+                const uint32_t w = (uint32_t)(code >> 32), ps = (uint32_t)code;
+                CHECK(w >= c.sbegin && w < c.sbegin + c.scount);
+                CHECK(ps >= prev_pass);
+                prev_pass = ps;
+                if (w < pl.singles.size()) CHECK(ps < pl.single_task_off[w + 1] - pl.single_task_off[w]);
+                seen_tasks.insert(code);
+            }
+            CHECK(seen_tasks.size() == pl.single_task_off[c.sbegin + c.scount] - pl.single_task_off[c.sbegin]);
         }
     }
     for (size_t k = 0; k + 1 < pl.duals.size(); k += 2) {
@@ -201,7 +237,7 @@ void plan_worker(uint64_t seed, int iters) {
         const int type = (int)(splitmix(s) % 3);
         const int ma = 1 + (int)(splitmix(s) % 3), mi = -(int)(splitmix(s) % 3), g = -(int)(splitmix(s) % 3);
         const uint64_t budget = (splitmix(s) & 1) ? (1ull << 40) : 4096ull + splitmix(s) % (64ull << 20);
-        const uint32_t flags = (uint32_t)(splitmix(s) % 8);
+        const uint32_t flags = (uint32_t)(splitmix(s) % 8) | ((splitmix(s) & 1) ? 32u : 0u);
         const bool cig = splitmix(s) % 4 != 0;
         ta::Plan pl;
         const uint32_t quantum = (splitmix(s) & 1) ? 1024u : (uint32_t)(splitmix(s) % 9);

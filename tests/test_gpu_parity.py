@@ -9,7 +9,7 @@ import pytest
 from conftest import DIGESTS, ROOT, STRIDED, cigar_digest, digest_batch, load_digest, run_plan
 
 from bioinfo1_amd import synth
-from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2, Aligner, DevicePlan,
+from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_SERIAL_PASSES, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2, Aligner, DevicePlan,
                                 align)
 from oracle.pyoracle import Oracle
 
@@ -147,7 +147,8 @@ def test_dual_fuzz(aligner, oracle, case):
     plan.close()
     want = oracle.align_batch(b, mode, *sc, True)
     # packed kernels (default), the int32 kernel alone (fused / separate walk)
-    for flags in (0, TA_PLAN_WALK1, TA_PLAN_WALK2, TA_PLAN_INT32_ONLY, TA_PLAN_INT32_ONLY | TA_PLAN_UNFUSED):
+    for flags in (0, TA_PLAN_WALK1, TA_PLAN_WALK2, TA_PLAN_INT32_ONLY, TA_PLAN_INT32_ONLY | TA_PLAN_UNFUSED,
+                  TA_PLAN_INT32_ONLY | TA_PLAN_SERIAL_PASSES):
         for cig in (True, False):
             got = run_plan(aligner, b, mode, sc, cig, flags)
             np.testing.assert_array_equal(got.scores, want.scores)
@@ -761,3 +762,38 @@ def test_host_pipeline(aligner, oracle):
             np.testing.assert_array_equal(r.target_begins, want.target_begins)
             if cig:
                 assert r.cigars() == want.cigars()
+
+
+@pytest.mark.gpu
+def test_int32_pass_pipeline(aligner, oracle):
+    """Multi-pass int32 pairs run one wave per (pair, pass) (fill_pipe_kernel,
+    fill_combine_kernel): local pairs past flex_local_fits (scores beyond the
+    int16 range, the natural int32 case), a 69-pass query, empty and one-pass
+    pairs in the same chunk, several chunks; against the oracle and against the
+    serial-pass fill (TA_PLAN_SERIAL_PASSES)."""
+    rel = synth.related_batch(3, 6500, 6400, seed=0x1F7)
+    rng = np.random.default_rng(0x1F8)
+    al = np.frombuffer(b"ACGT", np.uint8)
+
+    def rnd(k):
+        return al[rng.integers(4, size=k)].tobytes()
+
+    pairs = [(rel.query(p), rel.target(p)) for p in range(3)]
+    pairs += [(rnd(70000), rnd(200)), (b"", rnd(50)), (rnd(40), b""), (rnd(900), rnd(1200)), (rnd(3000), rnd(2500)),
+              (rnd(2049), rnd(64))]
+    b = synth.from_pairs(pairs)
+    for mode, sc in ((1, (5, -4, -4)), (0, (1, -1, -1)), (2, (2, -1, -1)), (1, (1, -1, -1))):
+        want = oracle.align_batch(b, mode, *sc, True)
+        if sc[0] == 5:  # the long local pairs leave the packed kernels: pipelined, walk in its own kernel
+            plan = DevicePlan(aligner, b, mode, *sc, True)
+            assert not plan.fused and plan.dual_pairs < b.n_pairs
+            plan.close()
+        for flags, budget in ((0, 0), (TA_PLAN_INT32_ONLY, 0), (TA_PLAN_INT32_ONLY, 1 << 20),
+                              (TA_PLAN_INT32_ONLY | TA_PLAN_SERIAL_PASSES, 0)):
+            for cig in (True, False):
+                got = run_plan(aligner, b, mode, sc, cig, flags, budget=budget)
+                np.testing.assert_array_equal(got.scores, want.scores)
+                np.testing.assert_array_equal(got.target_begins, want.target_begins)
+                if cig:
+                    for p in range(b.n_pairs):
+                        assert got.cigar(p) == want.cigar(p), (mode, sc, flags, budget, p)
