@@ -83,6 +83,11 @@ struct AffArgs {
     uint32_t epoch;    // tag base of this launch's records
     uint32_t* err;     // a poll gave up (never on a correct schedule)
     void* pout;        // PassOut[2] per (pass, couple): [(pass * count + w) * 2 + h]
+    // the pipelined int32 fill of multi-pass singles (affine_pipe_kernel): per
+    // single its first task, tasks in ticket order (single << 32 | pass),
+    // pout = PassOut per task; ticket, n_tasks and err as above
+    const uint32_t* task_off;
+    const uint64_t* tasks64;
 };
 
 // 64 boundary entries per chunk: column 64k+lane+1.
@@ -91,12 +96,50 @@ __device__ __forceinline__ int2 load_bchunk2(const int2* B, uint32_t m, uint32_t
     return j <= m ? B[j] : make_int2(0, kNeg);
 }
 
+// The pass boundary row (H, F per column).  A wave sweeping all of a pair's
+// passes keeps it in place (B).  The pipelined fill (one wave per (pair,
+// pass), affine_pipe_kernel) hands it over as two 8-byte records per column,
+// tag << 32 | H and tag << 32 | F, two buffers by pass parity, relaxed
+// agent-scope stores polled 64 columns at a time (as the linear int32 fill).
+struct AffBnd {
+    int2* B;
+    uint64_t* rec_w;        // null: B (or the last pass)
+    const uint64_t* rec_r;  // null: B (or pass 0)
+    uint32_t tag_w, tag_r;
+    uint32_t* err;
+};
+
+typedef __attribute__((address_space(1))) unsigned long long gu64a;
+
+__device__ __forceinline__ int2 load_bnd2(const AffBnd& io, uint32_t m, uint32_t k, int lane) {
+    if (!io.rec_r) return load_bchunk2(io.B, m, k, lane);
+    const uint32_t j = k * 64u + (uint32_t)lane + 1u;
+    const gu64a* r = (const gu64a*)(io.rec_r + 2ull * j);
+    int2 v = make_int2(0, kNeg);
+    for (uint32_t spins = 0;; ++spins) {
+        bool ok = true;
+        if (j <= m) {
+            const uint64_t x = __hip_atomic_load(r, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t y = __hip_atomic_load(r + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            ok = (uint32_t)(x >> 32) == io.tag_r && (uint32_t)(y >> 32) == io.tag_r;
+            v = make_int2((int)(uint32_t)x, (int)(uint32_t)y);
+        }
+        if (__builtin_amdgcn_ballot_w64(!ok) == 0) break;
+        if (spins > (1u << 22)) {  // bounded: the kernel always ends
+            if (lane == 0) atomicOr(io.err, 1u);
+            break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+    }
+    return v;
+}
+
 // One pass = rows row_base+1 .. row_base+nrows against the whole target.
 //   QDASH  some query row of this pass is '-' (its vertical gap steps are free)
 //   ROWSEL semi-global last pass whose row n is not the last register
 template <int MODE, bool CIGAR, bool QDASH, bool ROWSEL>
 __device__ __forceinline__ PassOut aff_pass(const AffArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
-                                            uint32_t m, uint32_t pass, bool last_pass, uint2* ptrs, int2* B,
+                                            uint32_t m, uint32_t pass, bool last_pass, uint2* ptrs, const AffBnd& B,
                                             int lane) {
     constexpr int R = kRows;
     const int O = a.open, X = a.extend, OX = wadd(a.open, a.extend);
@@ -156,8 +199,8 @@ __device__ __forceinline__ PassOut aff_pass(const AffArgs& a, const uint8_t* Q, 
     uint32_t tcur = load_tchunk(T, m, 0, lane), tnext = load_tchunk(T, m, 1, lane);
     int2 bcur = make_int2(0, kNeg), bnext = make_int2(0, kNeg);
     if (pass > 0) {
-        bcur = load_bchunk2(B, m, 0, lane);
-        bnext = load_bchunk2(B, m, 1, lane);
+        bcur = load_bnd2(B, m, 0, lane);
+        bnext = load_bnd2(B, m, 1, lane);
     }
     const uint32_t steps = m + nl - 1;
     uint2* prow = CIGAR ? ptrs + (uint64_t)pass * Tmax * kWave : nullptr;
@@ -175,7 +218,7 @@ __device__ __forceinline__ PassOut aff_pass(const AffArgs& a, const uint8_t* Q, 
         } else {
             if ((t & 63u) == 0 && t) {
                 bcur = bnext;
-                bnext = load_bchunk2(B, m, (t >> 6) + 1, lane);
+                bnext = load_bnd2(B, m, (t >> 6) + 1, lane);
             }
             topH = rdlane(bcur.x, t & 63u);
             topF = rdlane(bcur.y, t & 63u);
@@ -244,7 +287,17 @@ __device__ __forceinline__ PassOut aff_pass(const AffArgs& a, const uint8_t* Q, 
                     }
                 }
             }
-            if (has_next && (uint32_t)lane == nl - 1) B[j] = make_int2(H[R - 1], Flast);
+            if (has_next && (uint32_t)lane == nl - 1) {
+                if (B.rec_w) {
+                    const uint64_t tg = (uint64_t)B.tag_w << 32;
+                    __hip_atomic_store((gu64a*)(B.rec_w + 2ull * j), tg | (uint32_t)H[R - 1], __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                    __hip_atomic_store((gu64a*)(B.rec_w + 2ull * j + 1), tg | (uint32_t)Flast, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                } else {
+                    B.B[j] = make_int2(H[R - 1], Flast);
+                }
+            }
         }
         if constexpr (CIGAR) prow[t * kWave + lane] = make_uint2((accD << 16) | accI, (accF << 16) | accE);
     };
@@ -291,8 +344,8 @@ __device__ __forceinline__ PassOut aff_pass(const AffArgs& a, const uint8_t* Q, 
 
 template <int MODE, bool CIGAR>
 __device__ __forceinline__ PassOut aff_pass_any(const AffArgs& a, const uint8_t* Q, const uint8_t* T, uint32_t n,
-                                                uint32_t m, uint32_t pass, bool last_pass, uint2* ptrs, int2* B,
-                                                int lane) {
+                                                uint32_t m, uint32_t pass, bool last_pass, uint2* ptrs,
+                                                const AffBnd& B, int lane) {
     bool dash = false;
     const uint32_t row0 = pass * kPassRows + (uint32_t)lane * kRows;
 #pragma unroll
@@ -339,7 +392,7 @@ __global__ __launch_bounds__(kBlock) void affine_fill_kernel(AffArgs a) {
     const uint8_t* T = a.tbytes + a.toff[p];
     const uint32_t passes = n_passes(n);
     uint2* ptrs = CIGAR ? a.ptrs + a.ptr_off[p] : nullptr;
-    int2* B = (passes > 1) ? a.bnd + a.bnd_off[p] : nullptr;
+    const AffBnd B{(passes > 1) ? a.bnd + a.bnd_off[p] : nullptr, nullptr, nullptr, 0, 0, nullptr};
 
     int best_h = (MODE == kSemi) ? 0 : INT_MIN;  // semi starts from (0,m), cost 0
     uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
@@ -366,6 +419,82 @@ __global__ __launch_bounds__(kBlock) void affine_fill_kernel(AffArgs a) {
         a.goal_i[p] = (MODE == kGlobal) ? n : best_i;
         a.goal_j[p] = (MODE == kGlobal) ? m : best_j;
     }
+}
+
+// The pipelined int32 fill: one wave per (pair, pass) of a chunk's singles,
+// pass-major tickets (the planner's single_tasks), so the pass a wave polls
+// belongs to a wave that took an earlier ticket and is running; the passes'
+// results are folded by affine_fill_combine_kernel (as affine_fill_kernel).
+template <int MODE, bool CIGAR>
+__global__ __launch_bounds__(kBlock) void affine_pipe_kernel(AffArgs a) {
+    const int lane = threadIdx.x & 63;
+    uint32_t tk = 0;
+    if (lane == 0) tk = atomicAdd(a.ticket, 1u);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+    if (tk >= a.n_tasks) return;
+    const uint64_t code = a.tasks64[a.task_off[a.begin] + tk];
+    const uint32_t w = (uint32_t)(code >> 32), pass = (uint32_t)code;
+    const uint32_t p = a.order[w];
+    const uint32_t n = a.qlen[p], m = a.tlen[p];  // both > 0: empty pairs have no task
+    const bool last_pass = pass + 1 == n_passes(n);
+    uint64_t* rec = reinterpret_cast<uint64_t*>(a.bnd + a.bnd_off[p]);  // 2 buffers x 2 (m + 1) records
+    const uint64_t rb = 2ull * ((uint64_t)m + 1);
+    // tags: pass + 1 for pass p's row (never 0; the host zeroes the records before the launch)
+    const AffBnd B{nullptr, last_pass ? nullptr : rec + (pass & 1u) * rb, pass ? rec + ((pass - 1u) & 1u) * rb : nullptr,
+                   pass + 1u, pass, a.err};
+    uint2* ptrs = CIGAR ? a.ptrs + a.ptr_off[p] : nullptr;
+    const PassOut o = aff_pass_any<MODE, CIGAR>(a, a.qbytes + a.qoff[p], a.tbytes + a.toff[p], n, m, pass, last_pass,
+                                                ptrs, B, lane);
+    if (lane == 0) static_cast<PassOut*>(a.pout)[a.task_off[w] + pass] = o;
+}
+
+template <int MODE>
+__global__ void affine_fill_combine_kernel(AffArgs a) {
+    const uint32_t w = a.begin + blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= a.begin + a.count) return;
+    const uint32_t p = a.order[w];
+    const uint32_t n = a.qlen[p], m = a.tlen[p];
+    const int O = a.open, X = a.extend;
+    int score = 0;
+    uint32_t gi = 0, gj = 0, tb = 0;
+    if (n == 0 || m == 0) {  // closed forms of the empty loops (affine boundaries)
+        if (MODE == kGlobal) {
+            gi = n;
+            gj = m;
+            score = (n || m) ? wadd(O, wmul(n ? n : m, X)) : 0;
+        } else if (MODE == kLocal) {
+            tb = 1;
+        } else {
+            gj = (n == 0) ? m : 0;
+        }
+    } else {
+        const PassOut* po = static_cast<const PassOut*>(a.pout) + a.task_off[w];
+        const uint32_t passes = a.task_off[w + 1] - a.task_off[w];
+        int best_h = (MODE == kSemi) ? 0 : INT_MIN, corner = 0;
+        uint32_t best_i = 0, best_j = (MODE == kSemi) ? m : 0;
+        for (uint32_t k = 0; k < passes; ++k) {
+            const PassOut& o = po[k];
+            if (MODE != kGlobal && o.h > best_h) {
+                best_h = o.h;
+                best_i = o.i;
+                best_j = o.j;
+            }
+            if (MODE == kSemi && k + 1 == passes && o.row_h > best_h) {
+                best_h = o.row_h;
+                best_i = n;
+                best_j = o.row_j;
+            }
+            if (MODE == kGlobal && k + 1 == passes) corner = o.corner;
+        }
+        score = (MODE == kGlobal) ? corner : best_h;
+        tb = (MODE == kLocal) ? best_j + 1 : 0;
+        gi = (MODE == kGlobal) ? n : best_i;
+        gj = (MODE == kGlobal) ? m : best_j;
+    }
+    a.score[p] = score;
+    a.target_begin[p] = tb;
+    a.goal_i[p] = gi;
+    a.goal_j[p] = gj;
 }
 
 // The three-state walk (oracle/affine_oracle.c): H-state follows the source
@@ -897,6 +1026,25 @@ hipError_t launch_affine_dual(int mode, bool cigar, const AffArgs& a, hipStream_
 hipError_t launch_affine_fill(int mode, bool cigar, const AffArgs& a, hipStream_t s) {
     if (a.count == 0) return hipSuccess;
     const dim3 g = aff_grid(a.count), b(kBlock);
+    if (a.tasks64) {  // one wave per (pair, pass), then the fold of the passes
+        const dim3 gt = aff_grid(a.n_tasks), gc((a.count + 255) / 256), bc(256);
+#define TA_AFF_PIPE(M)                                                                                   \
+    case M:                                                                                              \
+        if (a.n_tasks) {                                                                                 \
+            if (cigar) hipLaunchKernelGGL((affine_pipe_kernel<M, true>), gt, b, 0, s, a);                \
+            else hipLaunchKernelGGL((affine_pipe_kernel<M, false>), gt, b, 0, s, a);                     \
+        }                                                                                                \
+        hipLaunchKernelGGL(affine_fill_combine_kernel<M>, gc, bc, 0, s, a);                              \
+        break;
+        switch (mode) {
+            TA_AFF_PIPE(kGlobal)
+            TA_AFF_PIPE(kLocal)
+            TA_AFF_PIPE(kSemi)
+            default: return hipErrorInvalidValue;
+        }
+#undef TA_AFF_PIPE
+        return hipGetLastError();
+    }
 #define TA_AFF_FILL(M)                                                                   \
     case M:                                                                              \
         if (cigar) hipLaunchKernelGGL((affine_fill_kernel<M, true>), g, b, 0, s, a);     \
@@ -939,6 +1087,9 @@ struct ta_affine_plan {
     uint64_t *d_ptr_off = nullptr, *d_bnd_off = nullptr, *d_slot_off = nullptr;
     uint32_t *d_err = nullptr, *d_tickets = nullptr;  // packed fill: poll error word, one ticket counter per chunk
     void* d_pout = nullptr;                           // PassOut[2] per (pass, couple) of one chunk
+    uint32_t* d_stask_off = nullptr;  // pipelined int32 fill: per single, its first task
+    uint64_t* d_stasks = nullptr;     // ... its tasks in ticket order
+    void* d_spout = nullptr;          // ... PassOut per task
 };
 
 namespace {
@@ -946,8 +1097,8 @@ namespace {
 using ta_host::fail;
 
 struct AffOffs {
-    uint64_t qlen, tlen, order, singles, duals, ptr_off, bnd_off, slot_off, err, tickets;  // uploaded
-    uint64_t goal_i, goal_j, fb, pout;                                                    // device-only
+    uint64_t qlen, tlen, order, singles, duals, stask_off, stasks, ptr_off, bnd_off, slot_off, err, tickets;  // uploaded
+    uint64_t goal_i, goal_j, fb, pout, spout;                                                               // device-only
 };
 
 // PassOut[2] per (pass, couple) of the largest chunk (24-byte PassOut)
@@ -969,11 +1120,13 @@ AffOffs aff_layout(const ta::AffinePlan& h, ta::BlockLayout& L) {
     o.order = L.add(avbytes(h.order));
     o.singles = L.add(avbytes(h.singles));
     o.duals = L.add(avbytes(h.duals));
+    o.stask_off = L.add(avbytes(h.single_task_off));
+    o.stasks = L.add(avbytes(h.single_tasks));
     o.ptr_off = L.add(avbytes(h.ptr_off));
     o.bnd_off = L.add(avbytes(h.bnd_off));
     o.slot_off = L.add(avbytes(h.slot_off));
     o.err = L.add(4);
-    o.tickets = L.add(4ull * h.chunks.size());
+    o.tickets = L.add(8ull * h.chunks.size());  // per chunk: packed, then pipelined int32
     return o;
 }
 
@@ -982,6 +1135,7 @@ void aff_layout_scratch(const ta::AffinePlan& h, ta::BlockLayout& L, AffOffs& o)
     o.goal_j = L.add(4ull * h.n_pairs);
     o.fb = L.add(4ull * (h.duals.size() + h.chunks.size()));
     o.pout = L.add(aff_pout_bytes(h));
+    o.spout = L.add(h.single_tasks.size() * 24ull);
 }
 
 void aff_pack(const ta::AffinePlan& h, const AffOffs& o, uint8_t* base) {
@@ -993,11 +1147,13 @@ void aff_pack(const ta::AffinePlan& h, const AffOffs& o, uint8_t* base) {
     put(o.order, h.order);
     put(o.singles, h.singles);
     put(o.duals, h.duals);
+    put(o.stask_off, h.single_task_off);
+    put(o.stasks, h.single_tasks);
     put(o.ptr_off, h.ptr_off);
     put(o.bnd_off, h.bnd_off);
     put(o.slot_off, h.slot_off);
     std::memset(base + o.err, 0, 4);
-    std::memset(base + o.tickets, 0, 4ull * h.chunks.size());
+    std::memset(base + o.tickets, 0, 8ull * h.chunks.size());
 }
 
 void aff_bind(ta_affine_plan* pl, uint8_t* d, const AffOffs& o) {
@@ -1017,6 +1173,9 @@ void aff_bind(ta_affine_plan* pl, uint8_t* d, const AffOffs& o) {
     pl->d_err = u32(o.err);
     pl->d_tickets = u32(o.tickets);
     pl->d_pout = d + o.pout;
+    pl->d_stask_off = u32(o.stask_off);
+    pl->d_stasks = u64(o.stasks);
+    pl->d_spout = d + o.spout;
 }
 
 // the oracle's range (oracle_affine_in_range): every |value| < 2^26
@@ -1086,6 +1245,9 @@ int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s,
     a.cigar_len = io->cigar_len;
     if (fill) {
         roctxRangePushA("ta affine fill");
+        // pass hand-off records start zeroed (tags are small integers; the region may hold old codes)
+        if ((ch.dcount && ch.dpasses > 1) || ch.spasses > 1)
+            TA_HIP(ctx, hipMemsetAsync(ctx->ws_bnd.p, 0, ch.bnd_entries * sizeof(int2), s));
         if (ch.dcount) {  // packed couples, then the couples they hand back, on the same stream
             uint32_t* fb_list = pl->d_fb + 2ull * ch.dbegin;
             uint32_t* fb_count = pl->d_fb + h.duals.size() + c;
@@ -1096,15 +1258,13 @@ int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s,
             d.count = ch.dcount;
             d.fb_list = fb_list;
             d.fb_count = fb_count;
-            // one wave per (couple, pass), tickets pass-major; the hand-off records
-            // start zeroed (tags are small integers; the region may hold old codes)
+            // one wave per (couple, pass), tickets pass-major
             d.ticket = pl->d_tickets + c;
             d.n_tasks = ch.dcount * ch.dpasses;
             d.epoch = ++ctx->epoch & 0x3FFFFFFu;
             d.err = pl->d_err;
             d.pout = pl->d_pout;
             TA_HIP(ctx, hipMemsetAsync(d.ticket, 0, 4, s));
-            if (ch.dpasses > 1) TA_HIP(ctx, hipMemsetAsync(ctx->ws_bnd.p, 0, ch.bnd_entries * sizeof(int2), s));
             TA_HIP(ctx, ta::launch_affine_dual(h.type, h.want_cigar, d, s));
             ta::AffArgs f = a;
             f.order = fb_list;
@@ -1117,6 +1277,15 @@ int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s,
         sa.order = pl->d_singles;
         sa.begin = ch.sbegin;
         sa.count = ch.scount;
+        if (ch.spasses > 1) {  // one wave per (pair, pass), tickets pass-major
+            sa.task_off = pl->d_stask_off;
+            sa.tasks64 = pl->d_stasks;
+            sa.ticket = pl->d_tickets + h.chunks.size() + c;
+            sa.n_tasks = h.single_task_off[ch.sbegin + ch.scount] - h.single_task_off[ch.sbegin];
+            sa.err = pl->d_err;
+            sa.pout = pl->d_spout;
+            TA_HIP(ctx, hipMemsetAsync(sa.ticket, 0, 4, s));
+        }
         TA_HIP(ctx, ta::launch_affine_fill(h.type, h.want_cigar, sa, s));
         roctxRangePop();
     }
@@ -1151,9 +1320,11 @@ struct AffineHostPlan final : ta_host::HostPlan {
         return affine_exec(pl, io, s, UINT32_MAX, true, true);
     }
     uint64_t slots_bytes() const override { return pl->h.slots_bytes; }
-    uint64_t err_offset() const override { return pl->h.duals.empty() ? UINT64_MAX : o.err; }
+    uint64_t err_offset() const override {
+        return pl->h.duals.empty() && pl->h.single_tasks.empty() ? UINT64_MAX : o.err;
+    }
     const char* err_message() const override {
-        return "packed affine fill: a pass hand-off poll timed out; results of this batch are invalid";
+        return "affine fill: a pass hand-off poll timed out; results of this batch are invalid";
     }
 };
 
@@ -1202,14 +1373,14 @@ uint64_t ta_affine_plan_cigar_slots_bytes(const ta_affine_plan* pl) { return pl 
 
 int ta_affine_plan_check(ta_affine_plan* pl) {
     if (!pl) return TA_ERR_ARG;
-    if (pl->h.duals.empty()) return TA_OK;
+    if (pl->h.duals.empty() && pl->h.single_tasks.empty()) return TA_OK;
     uint32_t err = 0;
     TA_HIP(pl->ctx, hipSetDevice(pl->ctx->device));
     TA_HIP(pl->ctx, hipMemcpy(&err, pl->d_err, 4, hipMemcpyDeviceToHost));
     if (!err) return TA_OK;
     TA_HIP(pl->ctx, hipMemset(pl->d_err, 0, 4));
     return fail(pl->ctx, TA_ERR_DEVICE,
-                "packed affine fill: a pass hand-off poll timed out; results of this plan are invalid");
+                "affine fill: a pass hand-off poll timed out; results of this plan are invalid");
 }
 uint64_t ta_affine_plan_workspace_bytes(const ta_affine_plan* pl) {
     return pl ? pl->h.ws_ptr_entries * sizeof(uint2) + pl->h.ws_bnd_entries * sizeof(int2) : 0;

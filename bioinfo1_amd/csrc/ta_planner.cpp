@@ -434,17 +434,20 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
     const uint64_t budget_entries = std::max<uint64_t>(budget / 8, 1);
     pl.ptr_off.assign(n_pairs, 0);
     pl.bnd_off.assign(n_pairs, 0);
-    AffinePlan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0, 0};
+    AffinePlan::Chunk c{0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
     auto unit_codes = [&](size_t k) -> uint64_t {
         const auto& u = units[k];
         if (!want_cigar) return 0;
         return ptr_dwords(qlen[u.first], tlen[u.first]) +
                (u.second == UINT32_MAX ? 0 : ptr_dwords(qlen[u.second], tlen[u.second]));
     };
-    // the packed fill runs one wave per (couple, pass); the int32 fill one per pair
+    // the packed fill runs one wave per (couple, pass); the int32 fill one per
+    // pair, or one per (pair, pass) when pipelined
+    const bool pipe_singles = !(flags & kPlanSerialPasses);
     auto unit_waves = [&](size_t k) -> uint64_t {
         const auto& u = units[k];
-        return u.second == UINT32_MAX ? 1 : n_passes(qlen[u.first]);
+        if (u.second == UINT32_MAX && !(pipe_singles && qlen[u.first] && tlen[u.first])) return 1;
+        return n_passes(qlen[u.first]);
     };
     const std::vector<size_t> starts = chunk_starts(units.size(), budget_entries, wave_quantum, unit_codes, unit_waves);
     size_t next_cut = 1;
@@ -454,7 +457,7 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
         const int cnt = u.second == UINT32_MAX ? 1 : 2;
         if (next_cut < starts.size() && k == starts[next_cut]) {
             pl.chunks.push_back(c);
-            c = {(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0, (uint32_t)(pl.duals.size() / 2), 0, 0, 0, 0};
+            c = {(uint32_t)pl.order.size(), 0, (uint32_t)pl.singles.size(), 0, (uint32_t)(pl.duals.size() / 2), 0, 0, 0, 0, 0};
             ++next_cut;
         }
         for (int h = 0; h < cnt; ++h) {
@@ -467,6 +470,8 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
             // boundary row for the int32 fallback ('-' in a query)
             uint64_t bw = bnd_words(qlen[p], tlen[p]);
             if (cnt == 2 && h == 0 && n_passes(qlen[p]) > 1) bw = std::max<uint64_t>(bw, 4ull * ((uint64_t)tlen[p] + 1));
+            // a pipelined single: its own records, the same 4 entries per column
+            if (cnt == 1 && pipe_singles && n_passes(qlen[p]) > 1) bw = std::max<uint64_t>(bw, 4ull * ((uint64_t)tlen[p] + 1));
             c.bnd_entries += bw;
             pl.order.push_back(p);
             ++c.count;
@@ -479,9 +484,26 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
         } else {
             pl.singles.push_back(u.first);
             ++c.scount;
+            if (pipe_singles && qlen[u.first] && tlen[u.first]) c.spasses = std::max(c.spasses, n_passes(qlen[u.first]));
         }
     }
     if (c.count) pl.chunks.push_back(c);
+    bool piped = false;
+    for (const auto& ch : pl.chunks) piped |= ch.spasses > 1;
+    if (piped) {
+        pl.single_task_off.assign(1, 0);
+        for (uint32_t p : pl.singles)
+            pl.single_task_off.push_back(pl.single_task_off.back() + (qlen[p] && tlen[p] ? n_passes(qlen[p]) : 0));
+        pl.single_tasks.assign(pl.single_task_off.back(), 0ull);
+        for (const auto& ch : pl.chunks) {
+            if (ch.spasses < 2) continue;
+            uint32_t at = pl.single_task_off[ch.sbegin];
+            for (uint32_t ps = 0; ps < ch.spasses; ++ps)
+                for (uint32_t w = ch.sbegin; w < ch.sbegin + ch.scount; ++w)
+                    if (pl.single_task_off[w + 1] - pl.single_task_off[w] > ps)
+                        pl.single_tasks[at++] = ((uint64_t)w << 32) | ps;
+        }
+    }
     for (const auto& ch : pl.chunks) {
         pl.ws_ptr_entries = std::max(pl.ws_ptr_entries, ch.ptr_entries);
         pl.ws_bnd_entries = std::max(pl.ws_bnd_entries, ch.bnd_entries);

@@ -93,8 +93,12 @@ struct AffinePlan {
         uint32_t dbegin, dcount;  // couples
         uint64_t ptr_entries, bnd_entries;
         uint32_t dpasses;         // largest pass count of the chunk's couples (one wave per couple and pass)
+        uint32_t spasses;         // largest pass count of the singles (> 1: one wave per pair and pass)
     };
     std::vector<Chunk> chunks;
+    // pipelined int32 fill of multi-pass singles, as Plan::single_task_off / single_tasks
+    std::vector<uint32_t> single_task_off;
+    std::vector<uint64_t> single_tasks;
     uint64_t slots_bytes = 0, ws_ptr_entries = 0, ws_bnd_entries = 0;
 };
 

@@ -43,4 +43,24 @@ for name, b in cases:
         plan.close()
         print("%-26s %-9s %9.2f ms  %7.1f GCUPS" % (name, label, ms, cells / ms / 1e6), flush=True)
     assert (res["serial"][0] == res["pipelined"][0]).all() and res["serial"][1] == res["pipelined"][1], name
+# affine-gap local (the affine packed fill takes global / semi only: every local pair is an int32 single)
+for name, b in (("affine local 16 x 10kb", synth.related_batch(16, 10000, 10000, seed=21)),
+                ("affine local 1024 x 10kb", synth.related_batch(1024, 10000, 10000, seed=22))):
+    cells = float(sum(int(b.qlen[p]) * int(b.tlen[p]) for p in range(b.n_pairs)))
+    res = {}
+    for label, flags in (("serial", TA_PLAN_SERIAL_PASSES), ("pipelined", 0)):
+        plan = DevicePlan(al, b, 1, 2, -3, -1, True, gap_open=-5, flags=flags)
+        plan.run()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            plan.run()
+        torch.cuda.synchronize()
+        ms = (time.perf_counter() - t0) / 3 * 1e3
+        r = plan.results()
+        res[label] = (r.scores.copy(), [r.cigar(p) for p in range(min(b.n_pairs, 64))])
+        plan.check()
+        plan.close()
+        print("%-26s %-9s %9.2f ms  %7.1f GCUPS" % (name, label, ms, cells / ms / 1e6), flush=True)
+    assert (res["serial"][0] == res["pipelined"][0]).all() and res["serial"][1] == res["pipelined"][1], name
 print("pipelined == serial on every batch")

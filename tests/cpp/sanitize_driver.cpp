@@ -218,6 +218,30 @@ void check_affine(const ta::AffinePlan& pl) {
         CHECK(c.ptr_entries <= pl.ws_ptr_entries);
     }
     CHECK(count == P);
+    bool piped = false;
+    for (const auto& c : pl.chunks) piped |= c.spasses > 1;
+    CHECK(piped == !pl.single_task_off.empty());
+    if (piped) {
+        CHECK(pl.single_task_off.size() == pl.singles.size() + 1);
+        for (const auto& c : pl.chunks) {
+            if (c.spasses < 2) continue;
+            uint32_t prev_pass = 0;
+            std::set<uint64_t> seen_tasks;
+            for (uint32_t w = c.sbegin; w < c.sbegin + c.scount; ++w) {
+                const uint32_t x = pl.singles[w];
+                if (ta::n_passes(pl.qlen[x]) > 1 && pl.tlen[x])
+                    CHECK(pl.bnd_off[x] + 4ull * (pl.tlen[x] + 1) <= c.bnd_entries);
+            }
+            for (uint32_t k = pl.single_task_off[c.sbegin]; k < pl.single_task_off[c.sbegin + c.scount]; ++k) {
+                const uint32_t w = (uint32_t)(pl.single_tasks[k] >> 32), ps = (uint32_t)pl.single_tasks[k];
+                CHECK(w >= c.sbegin && w < c.sbegin + c.scount && ps >= prev_pass);
+                prev_pass = ps;
+                if (w < pl.singles.size()) CHECK(ps < pl.single_task_off[w + 1] - pl.single_task_off[w]);
+                seen_tasks.insert(pl.single_tasks[k]);
+            }
+            CHECK(seen_tasks.size() == pl.single_task_off[c.sbegin + c.scount] - pl.single_task_off[c.sbegin]);
+        }
+    }
 }
 
 void plan_worker(uint64_t seed, int iters) {
@@ -244,7 +268,7 @@ void plan_worker(uint64_t seed, int iters) {
         ta::build_plan(pl, P, q.data(), t.data(), type, ma, mi, g, cig, budget, flags, quantum);
         check_linear(pl, budget);
         ta::AffinePlan ap;
-        ta::build_affine_plan(ap, P, q.data(), t.data(), type, ma, mi, -2, g, cig, budget, flags & 1u, quantum);
+        ta::build_affine_plan(ap, P, q.data(), t.data(), type, ma, mi, -2, g, cig, budget, flags & 33u, quantum);
         check_affine(ap);
     }
 }

@@ -12,7 +12,7 @@ import pytest
 from conftest import cigar_digest, digest_batch, load_digest, run_plan
 
 from bioinfo1_amd import synth
-from bioinfo1_amd.align import TA_PLAN_INT32_ONLY, Aligner, DevicePlan, align_affine
+from bioinfo1_amd.align import TA_PLAN_INT32_ONLY, TA_PLAN_SERIAL_PASSES, Aligner, DevicePlan, align_affine
 from oracle.pyoracle import Oracle, affine_cigar_check_batch
 
 pytestmark = pytest.mark.gpu
@@ -173,10 +173,37 @@ def test_affine_dual_fill(aligner, oracle, case):
     plan.close()
     want = oracle.align_affine_batch(b, mode, *sc, True)
     assert not want.status.any()
-    for flags in (0, TA_PLAN_INT32_ONLY):
+    for flags in (0, TA_PLAN_INT32_ONLY, TA_PLAN_INT32_ONLY | TA_PLAN_SERIAL_PASSES):
         got = run_plan(aligner, b, mode, (sc[0], sc[1], sc[3]), True, flags, gap_open=sc[2])
         _same(got, want, P, (case, flags))
         got0 = run_plan(aligner, b, mode, (sc[0], sc[1], sc[3]), False, flags, gap_open=sc[2])
         np.testing.assert_array_equal(got0.scores, want.scores)
     got = aligner.align_batch_affine(b, mode, *sc, True)  # host-memory batch
     _same(got, want, P, (case, "host"))
+
+
+def test_affine_int32_pass_pipeline(aligner, oracle):
+    """Affine multi-pass int32 pairs (every local pair; pairs past the packed
+    range) run one wave per (pair, pass) (affine_pipe_kernel,
+    affine_fill_combine_kernel): a 69-pass query, empty and one-pass pairs in
+    the same chunk, several chunks; against the oracle and the serial-pass fill."""
+    rel = synth.related_batch(2, 3000, 2900, seed=0xAF7)
+    rng = np.random.default_rng(0xAF8)
+    al = np.frombuffer(b"ACGT", np.uint8)
+
+    def rnd(k):
+        return al[rng.integers(4, size=k)].tobytes()
+
+    pairs = [(rel.query(p), rel.target(p)) for p in range(2)]
+    pairs += [(rnd(70000), rnd(150)), (b"", rnd(50)), (rnd(40), b""), (rnd(900), rnd(1200)), (rnd(2049), rnd(64))]
+    b = synth.from_pairs(pairs)
+    for mode, sc in ((1, (2, -3, -5, -1)), (0, (1, -1, -2, -1)), (2, (2, -3, -5, -2))):
+        want = oracle.align_affine_batch(b, mode, *sc, True)
+        assert not want.status.any()
+        for flags, budget in ((0, 0), (TA_PLAN_INT32_ONLY, 0), (TA_PLAN_INT32_ONLY, 1 << 20),
+                              (TA_PLAN_INT32_ONLY | TA_PLAN_SERIAL_PASSES, 0)):
+            got = run_plan(aligner, b, mode, (sc[0], sc[1], sc[3]), True, flags, gap_open=sc[2], budget=budget)
+            _same(got, want, b.n_pairs, (mode, flags, budget))
+            got0 = run_plan(aligner, b, mode, (sc[0], sc[1], sc[3]), False, flags, gap_open=sc[2], budget=budget)
+            np.testing.assert_array_equal(got0.scores, want.scores)
+            np.testing.assert_array_equal(got0.target_begins, want.target_begins)
