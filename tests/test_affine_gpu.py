@@ -207,3 +207,5 @@ def test_affine_int32_pass_pipeline(aligner, oracle):
             got0 = run_plan(aligner, b, mode, (sc[0], sc[1], sc[3]), False, flags, gap_open=sc[2], budget=budget)
             np.testing.assert_array_equal(got0.scores, want.scores)
             np.testing.assert_array_equal(got0.target_begins, want.target_begins)
+        got = aligner.align_batch_affine(b, mode, *sc, True)  # host-memory batch
+        _same(got, want, b.n_pairs, (mode, "host"))

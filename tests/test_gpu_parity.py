@@ -797,3 +797,10 @@ def test_int32_pass_pipeline(aligner, oracle):
                 if cig:
                     for p in range(b.n_pairs):
                         assert got.cigar(p) == want.cigar(p), (mode, sc, flags, budget, p)
+        got = aligner.align_batch(b, mode, *sc, True)  # host-memory batch (ta_align_batch)
+        np.testing.assert_array_equal(got.scores, want.scores)
+        for p in range(b.n_pairs):
+            assert got.cigar(p) == want.cigar(p), (mode, sc, "host", p)
+        # one pair per call (the drop-in's path for pairs the server does not take)
+        assert align(b.query(0), b.target(0), mode, *sc) == (int(want.scores[0]), want.cigar(0),
+                                                              int(want.target_begins[0]))
