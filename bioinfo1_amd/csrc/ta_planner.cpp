@@ -174,6 +174,29 @@ std::vector<size_t> chunk_starts(size_t n_units, uint64_t budget, uint32_t wave_
     return starts;
 }
 
+// Ticket order of one chunk's pass tasks (units first .. first+count-1, unit
+// w with off[w+1] - off[w] passes).  A task's predecessor (the same unit's
+// pass - 1) must hold an earlier ticket: its wave is then running, so every
+// poll ends.  Pass-major (start-aligned): every unit's pass 0, then every
+// pass 1, ...; the longest units' last passes get the last tickets and run
+// alone at the end of the launch.  End-aligned (default): level L = pass -
+// passes, ascending, so every unit's last pass is in the last level and the
+// long chains start first.  Within a level: plan order (most cells first).
+template <class Emit>
+void order_pass_tasks(const std::vector<uint32_t>& off, uint32_t first, uint32_t count, bool end_aligned, Emit emit) {
+    uint32_t maxp = 0;
+    for (uint32_t w = first; w < first + count; ++w) maxp = std::max(maxp, off[w + 1] - off[w]);
+    for (uint32_t lv = 0; lv < maxp; ++lv)
+        for (uint32_t w = first; w < first + count; ++w) {
+            const uint32_t P = off[w + 1] - off[w];
+            if (end_aligned) {
+                if (lv + P >= maxp) emit(w, lv + P - maxp);
+            } else if (lv < P) {
+                emit(w, lv);
+            }
+        }
+}
+
 }  // namespace
 
 void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type, int match,
@@ -372,13 +395,11 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     for (size_t w = 0; w < pl.flexes.size() / 2; ++w)
         pl.flex_task_off.push_back(pl.flex_task_off.back() + n_passes(qlen[pl.flexes[2 * w]]));
     pl.flex_tasks.assign(pl.flex_task_off.back(), 0u);
+    const bool end_aligned = !(flags & kPlanPassMajor);
     for (const auto& ch : pl.chunks) {
-        uint32_t at = pl.flex_task_off[ch.fbegin], maxp = 0;
-        for (uint32_t w = ch.fbegin; w < ch.fbegin + ch.fcount; ++w)
-            maxp = std::max(maxp, pl.flex_task_off[w + 1] - pl.flex_task_off[w]);
-        for (uint32_t ps = 0; ps < maxp; ++ps)
-            for (uint32_t w = ch.fbegin; w < ch.fbegin + ch.fcount; ++w)
-                if (pl.flex_task_off[w + 1] - pl.flex_task_off[w] > ps) pl.flex_tasks[at++] = w * 64u + ps;
+        uint32_t at = pl.flex_task_off[ch.fbegin];
+        order_pass_tasks(pl.flex_task_off, ch.fbegin, ch.fcount, end_aligned,
+                         [&](uint32_t w, uint32_t ps) { pl.flex_tasks[at++] = w * 64u + ps; });
     }
     if (piped) {
         pl.single_task_off.assign(1, 0);
@@ -388,10 +409,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         for (const auto& ch : pl.chunks) {
             if (ch.spasses < 2) continue;  // single-pass singles: the one-wave-per-pair fill
             uint32_t at = pl.single_task_off[ch.sbegin];
-            for (uint32_t ps = 0; ps < ch.spasses; ++ps)
-                for (uint32_t w = ch.sbegin; w < ch.sbegin + ch.scount; ++w)
-                    if (pl.single_task_off[w + 1] - pl.single_task_off[w] > ps)
-                        pl.single_tasks[at++] = ((uint64_t)w << 32) | ps;
+            order_pass_tasks(pl.single_task_off, ch.sbegin, ch.scount, end_aligned,
+                             [&](uint32_t w, uint32_t ps) { pl.single_tasks[at++] = ((uint64_t)w << 32) | ps; });
         }
     }
     for (const auto& c : pl.chunks) {
@@ -498,10 +517,8 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
         for (const auto& ch : pl.chunks) {
             if (ch.spasses < 2) continue;
             uint32_t at = pl.single_task_off[ch.sbegin];
-            for (uint32_t ps = 0; ps < ch.spasses; ++ps)
-                for (uint32_t w = ch.sbegin; w < ch.sbegin + ch.scount; ++w)
-                    if (pl.single_task_off[w + 1] - pl.single_task_off[w] > ps)
-                        pl.single_tasks[at++] = ((uint64_t)w << 32) | ps;
+            order_pass_tasks(pl.single_task_off, ch.sbegin, ch.scount, !(flags & kPlanPassMajor),
+                             [&](uint32_t w, uint32_t ps) { pl.single_tasks[at++] = ((uint64_t)w << 32) | ps; });
         }
     }
     for (const auto& ch : pl.chunks) {

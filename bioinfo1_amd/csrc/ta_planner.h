@@ -21,6 +21,7 @@ constexpr uint32_t kPlanUnfused = 4u;    // int32-only plans: traceback as its o
 constexpr uint32_t kPlanWalk1 = 8u;      // local walks: one pair per wave (traceback_pair)
 constexpr uint32_t kPlanWalk2 = 16u;     // local walks: two pairs per wave (ta_walk2.h), not lane walks
 constexpr uint32_t kPlanSerialPasses = 32u;  // int32 fill: one wave sweeps all of a pair's passes
+constexpr uint32_t kPlanPassMajor = 64u;     // pass tasks ticketed start-aligned (every pass 0 first)
 
 // Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);

@@ -156,6 +156,7 @@ int ta_align_batch_flags(ta_context* ctx, uint32_t n_pairs, const char* query_by
 #define TA_PLAN_WALK1 8u      /* local tracebacks: one pair per wave (run walk) */
 #define TA_PLAN_WALK2 16u     /* local tracebacks: two pairs per wave (run walk), not one lane per pair */
 #define TA_PLAN_SERIAL_PASSES 32u /* int32 fill: one wave sweeps all of a pair's passes (no pass pipelining) */
+#define TA_PLAN_PASS_MAJOR 64u    /* pass-pipelined fills: tickets start-aligned (every pass 0 first), not end-aligned */
 int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
                    const uint32_t* target_len_host, int type, int match, int mismatch, int gap, int want_cigar,
                    uint64_t workspace_budget, uint32_t flags, ta_plan** out);

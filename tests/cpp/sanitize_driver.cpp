@@ -152,12 +152,12 @@ void check_linear(const ta::Plan& pl, uint64_t budget) {
     std::set<uint32_t> tasks(pl.flex_tasks.begin(), pl.flex_tasks.end());
     CHECK(tasks.size() == pl.flex_tasks.size());
     for (const auto& c : pl.chunks) {
-        uint32_t prev_pass = 0;
+        std::set<uint32_t> done;  // a task's predecessor (same couple, pass - 1) has an earlier ticket
         for (uint32_t k = pl.flex_task_off[c.fbegin]; k < pl.flex_task_off[c.fbegin + c.fcount]; ++k) {
             const uint32_t w = pl.flex_tasks[k] / 64, ps = pl.flex_tasks[k] % 64;
             CHECK(w >= c.fbegin && w < c.fbegin + c.fcount);
-            CHECK(ps >= prev_pass);
-            prev_pass = ps;
+            if (ps) CHECK(done.count(pl.flex_tasks[k] - 1) == 1);
+            done.insert(pl.flex_tasks[k]);
             CHECK(ps < pl.flex_task_off[w + 1] - pl.flex_task_off[w]);
         }
     }
@@ -172,7 +172,7 @@ void check_linear(const ta::Plan& pl, uint64_t budget) {
         for (const auto& c : pl.chunks) {
             if (c.spasses < 2) continue;
             std::set<uint64_t> seen_tasks;
-            uint32_t prev_pass = 0, maxp = 0;
+            uint32_t maxp = 0;
             for (uint32_t w = c.sbegin; w < c.sbegin + c.scount; ++w) {
                 const uint32_t x = pl.singles[w];
                 const uint32_t want = pl.qlen[x] && pl.tlen[x] ? ta::n_passes(pl.qlen[x]) : 0;
@@ -185,8 +185,7 @@ void check_linear(const ta::Plan& pl, uint64_t budget) {
                 const uint64_t code = pl.single_tasks[k];
                 const uint32_t w = (uint32_t)(code >> 32), ps = (uint32_t)code;
                 CHECK(w >= c.sbegin && w < c.sbegin + c.scount);
-                CHECK(ps >= prev_pass);
-                prev_pass = ps;
+                if (ps) CHECK(seen_tasks.count(code - 1) == 1);  // predecessor ticketed earlier
                 if (w < pl.singles.size()) CHECK(ps < pl.single_task_off[w + 1] - pl.single_task_off[w]);
                 seen_tasks.insert(code);
             }
@@ -225,7 +224,6 @@ void check_affine(const ta::AffinePlan& pl) {
         CHECK(pl.single_task_off.size() == pl.singles.size() + 1);
         for (const auto& c : pl.chunks) {
             if (c.spasses < 2) continue;
-            uint32_t prev_pass = 0;
             std::set<uint64_t> seen_tasks;
             for (uint32_t w = c.sbegin; w < c.sbegin + c.scount; ++w) {
                 const uint32_t x = pl.singles[w];
@@ -234,8 +232,8 @@ void check_affine(const ta::AffinePlan& pl) {
             }
             for (uint32_t k = pl.single_task_off[c.sbegin]; k < pl.single_task_off[c.sbegin + c.scount]; ++k) {
                 const uint32_t w = (uint32_t)(pl.single_tasks[k] >> 32), ps = (uint32_t)pl.single_tasks[k];
-                CHECK(w >= c.sbegin && w < c.sbegin + c.scount && ps >= prev_pass);
-                prev_pass = ps;
+                CHECK(w >= c.sbegin && w < c.sbegin + c.scount);
+                if (ps) CHECK(seen_tasks.count(pl.single_tasks[k] - 1) == 1);  // predecessor ticketed earlier
                 if (w < pl.singles.size()) CHECK(ps < pl.single_task_off[w + 1] - pl.single_task_off[w]);
                 seen_tasks.insert(pl.single_tasks[k]);
             }
@@ -261,14 +259,14 @@ void plan_worker(uint64_t seed, int iters) {
         const int type = (int)(splitmix(s) % 3);
         const int ma = 1 + (int)(splitmix(s) % 3), mi = -(int)(splitmix(s) % 3), g = -(int)(splitmix(s) % 3);
         const uint64_t budget = (splitmix(s) & 1) ? (1ull << 40) : 4096ull + splitmix(s) % (64ull << 20);
-        const uint32_t flags = (uint32_t)(splitmix(s) % 8) | ((splitmix(s) & 1) ? 32u : 0u);
+        const uint32_t flags = (uint32_t)(splitmix(s) % 8) | ((splitmix(s) & 1) ? 32u : 0u) | ((splitmix(s) & 1) ? 64u : 0u);
         const bool cig = splitmix(s) % 4 != 0;
         ta::Plan pl;
         const uint32_t quantum = (splitmix(s) & 1) ? 1024u : (uint32_t)(splitmix(s) % 9);
         ta::build_plan(pl, P, q.data(), t.data(), type, ma, mi, g, cig, budget, flags, quantum);
         check_linear(pl, budget);
         ta::AffinePlan ap;
-        ta::build_affine_plan(ap, P, q.data(), t.data(), type, ma, mi, -2, g, cig, budget, flags & 33u, quantum);
+        ta::build_affine_plan(ap, P, q.data(), t.data(), type, ma, mi, -2, g, cig, budget, flags & 97u, quantum);
         check_affine(ap);
     }
 }
