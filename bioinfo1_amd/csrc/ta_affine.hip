@@ -88,6 +88,7 @@ struct AffArgs {
     // pout = PassOut per task; ticket, n_tasks and err as above
     const uint32_t* task_off;
     const uint64_t* tasks64;
+    uint32_t end_aligned;  // dual tickets: level = pass + (chunk passes - couple passes), not the pass
 };
 
 // 64 boundary entries per chunk: column 64k+lane+1.
@@ -896,8 +897,9 @@ __device__ __forceinline__ void aff_dual_pass_nv(const AffArgs& a, const uint8_t
 constexpr uint32_t kAffSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to the int32 fill
 
 // order: 2 pair ids per couple (same n and m, values within int16).  One wave
-// per (couple, pass): a wave takes the next ticket, pass-major (every couple's
-// pass 0, then every pass 1, ...), so the pass it polls belongs to a wave that
+// per (couple, pass): a wave takes the next ticket, level-major (level = pass,
+// or end-aligned pass + chunk passes - couple passes: ta_planner.cpp
+// order_pass_tasks), so the pass it polls belongs to a wave that
 // took an earlier ticket and is running -- every poll ends -- and a chunk of
 // long couples (config 5: 2,048 couples x 10 passes) fills every wave slot
 // instead of two per SIMD.  Each wave writes its pass's PassOut; a combine
@@ -909,12 +911,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     if (lane == 0) tk = atomicAdd(a.ticket, 1u);
     tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
     if (tk >= a.n_tasks) return;
-    const uint32_t pass = tk / a.count, w = tk - pass * a.count;
+    const uint32_t level = tk / a.count, w = tk - level * a.count;
     uint32_t p[2];
     p[0] = a.order[2 * (a.begin + w)];
     p[1] = a.order[2 * (a.begin + w) + 1];
     const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
     const uint32_t passes = n_passes(n);
+    const uint32_t shift = a.end_aligned ? a.n_tasks / a.count - passes : 0u;
+    if (level < shift) return;
+    const uint32_t pass = level - shift;
     if (pass >= passes) return;
     PassOut* po = static_cast<PassOut*>(a.pout) + 2ull * ((uint64_t)pass * a.count + w);
     const uint8_t* Q[2];
@@ -1264,6 +1269,7 @@ int affine_exec_chunk(ta_affine_plan* pl, const ta_device_io* io, hipStream_t s,
             d.epoch = ++ctx->epoch & 0x3FFFFFFu;
             d.err = pl->d_err;
             d.pout = pl->d_pout;
+            d.end_aligned = h.end_aligned ? 1u : 0u;
             TA_HIP(ctx, hipMemsetAsync(d.ticket, 0, 4, s));
             TA_HIP(ctx, ta::launch_affine_dual(h.type, h.want_cigar, d, s));
             ta::AffArgs f = a;

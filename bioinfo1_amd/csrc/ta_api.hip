@@ -236,6 +236,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
                     d.epoch = ++ctx->epoch & 0x3FFFFFFu;
                     d.err = pl->d_err;
                     d.pout = pl->d_dpout;
+                    d.end_aligned = h.end_aligned ? 1u : 0u;
                     TA_HIP(ctx, hipMemsetAsync(d.ticket, 0, 4, s));
                 }
                 if (ch.fcount) {  // beside the flexible fill: fork onto aux2 (after the counter reset), join below

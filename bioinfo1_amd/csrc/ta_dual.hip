@@ -403,8 +403,10 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
 constexpr uint32_t kDualSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to the int32 fill
 
 // Chunks of multi-pass couples (a.ticket set) run one wave per (couple, pass):
-// ticket t is pass t / count of couple t % count (pass-major), so the pass a
-// wave polls belongs to a wave that took an earlier ticket and is running;
+// ticket t is level t / count of couple t % count; the level is the pass
+// (pass-major) or, end-aligned (ta_planner.cpp order_pass_tasks), the pass
+// plus the chunk's pass count minus the couple's, so the pass a wave polls
+// belongs to a wave that took an earlier ticket and is running;
 // each wave writes its pass's PassOut and dual_combine_kernel folds them.
 // Otherwise one wave per couple sweeps its passes.
 template <int MODE, bool CIGAR>
@@ -417,7 +419,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
         if (lane == 0) tk = atomicAdd(a.ticket, 1u);
         tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
         if (tk >= a.n_tasks) return;
-        p_only = tk / a.count;
+        p_only = tk / a.count;  // the level; the pass once the couple's pass count is known
         widx = tk - p_only * a.count;
     } else {
         widx = wave_id();
@@ -428,6 +430,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     p[1] = a.order[2 * (a.begin + widx) + 1];
     const uint32_t n = a.qlen[p[0]], m = a.tlen[p[0]];
     const uint32_t passes = n_passes(n);
+    if (pipe && a.end_aligned) {
+        const uint32_t shift = a.n_tasks / a.count - passes;  // levels before this couple's pass 0
+        if (p_only < shift) return;
+        p_only -= shift;
+    }
     if (pipe && p_only >= passes) return;
     PassOut* po = pipe ? static_cast<PassOut*>(a.pout) + 2ull * ((uint64_t)p_only * a.count + widx) : nullptr;
     DualIo io;

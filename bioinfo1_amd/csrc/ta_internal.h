@@ -61,6 +61,9 @@ struct FillArgs {
     // pipelined int32 fill (fill_pipe_kernel; task_off = per single, ticket,
     // n_tasks, err, pout = PassOut per task as above): ticket order, single << 32 | pass
     const uint64_t* tasks64;
+    // multi-pass dual chunks: ticket t = level t / count of couple t % count;
+    // pass = level (pass-major) or level - (chunk passes - couple passes) (end-aligned)
+    uint32_t end_aligned;
 };
 
 struct TraceArgs {

@@ -396,6 +396,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         pl.flex_task_off.push_back(pl.flex_task_off.back() + n_passes(qlen[pl.flexes[2 * w]]));
     pl.flex_tasks.assign(pl.flex_task_off.back(), 0u);
     const bool end_aligned = !(flags & kPlanPassMajor);
+    pl.end_aligned = end_aligned;
     for (const auto& ch : pl.chunks) {
         uint32_t at = pl.flex_task_off[ch.fbegin];
         order_pass_tasks(pl.flex_task_off, ch.fbegin, ch.fcount, end_aligned,
@@ -430,6 +431,7 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
     pl.open = gap_open;
     pl.extend = gap_extend;
     pl.want_cigar = want_cigar;
+    pl.end_aligned = !(flags & kPlanPassMajor);
     pl.qlen.assign(qlen, qlen + n_pairs);
     pl.tlen.assign(tlen, tlen + n_pairs);
     const std::vector<uint32_t> byc = by_cells(n_pairs, qlen, tlen);

@@ -39,6 +39,7 @@ struct Plan {
     bool want_cigar = false;
     bool wide = false;   // local mode with |values| that could reach 2^25: unscaled int32 kernel
     bool fused = false;  // int32-only plans: the fill kernel walks its own pair
+    bool end_aligned = true;  // pass tasks ticketed end-aligned (not kPlanPassMajor)
     // local walks: 16 = lane walks (ta_walk_lane.h), 32 = two pairs per wave
     // (ta_walk2.h), 0 = one pair per wave (traceback_pair)
     int walk_group = 16;
@@ -83,6 +84,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
 struct AffinePlan {
     uint32_t n_pairs = 0;
     int type = 0, match = 0, mismatch = 0, open = 0, extend = 0;
+    bool end_aligned = true;  // pass tasks ticketed end-aligned (not kPlanPassMajor)
     bool want_cigar = false;
     std::vector<uint32_t> qlen, tlen;
     std::vector<uint32_t> order;           // pairs by descending cells: the big ones start first
