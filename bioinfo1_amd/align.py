@@ -146,7 +146,7 @@ ABI_SYMBOLS = [
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
     "ta_affine_plan_execute_traceback", "ta_affine_plan_check", "ta_align_batch_affine",
     "ta_server_create", "ta_server_destroy", "ta_server_fits", "ta_server_align", "ta_server_running",
-    "ta_server_last_times",
+    "ta_server_last_times", "ta_server_pause", "ta_server_resume",
 ]
 # The drop-in C++ entry point (team_alignment.hpp), g++/libstdc++ cxx11 mangling.
 TEAM_ALIGN_SYMBOL = ("_ZN4team5AlignEPKcjS1_jNS_13AlignmentTypeEiiiPNSt7__cxx1112basic_stringIcSt11char_traitsIcESaIcEEEPj")

@@ -239,14 +239,16 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         const uint32_t n = qlen[p], m = tlen[p];
         // (equal shapes within int16 stay on the dual fill even when multi-pass: measured faster
         // than the pipelined flexible fill on config 5, 4,056 vs 3,765 GCUPS)
+        // (< 64 passes: the hand-off tags epoch * 64 + pass + 1 never wrap to 0, ta_dual.hip)
         const bool couple = dual && k + 1 < n_pairs && qlen[order[k + 1]] == n && tlen[order[k + 1]] == m &&
-                            fits_int16(type, n, m, match, mismatch, gap);
+                            n_passes(n) < 64 && fits_int16(type, n, m, match, mismatch, gap);
         // A lone pair (one-pair batches: the drop-in call) runs coupled with
         // itself in the packed kernel -- both halves compute it, its codes are
         // written once -- whose wave and lane walk finish sooner than one int32
         // wave walking inside the fill, except for tiny pairs where the one
         // fused launch wins.
-        const bool self = dual && n_pairs == 1 && (uint64_t)n * m >= 4096 && fits_int16(type, n, m, match, mismatch, gap);
+        const bool self = dual && n_pairs == 1 && (uint64_t)n * m >= 4096 && n_passes(n) < 64 &&
+                          fits_int16(type, n, m, match, mismatch, gap);
         if (couple) {
             units.push_back({1, p, order[k + 1], (uint64_t)n * m});
             k += 2;
@@ -443,6 +445,7 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
     for (uint32_t k = 0; k < n_pairs;) {
         const uint32_t x = byc[k];
         if (dual_ok && k + 1 < n_pairs && qlen[byc[k + 1]] == qlen[x] && tlen[byc[k + 1]] == tlen[x] &&
+            n_passes(qlen[x]) < 64 &&  // hand-off tags epoch * 64 + pass + 1 never wrap (ta_affine.hip)
             affine_fits_int16(type, qlen[x], tlen[x], match, mismatch, gap_open, gap_extend)) {
             units.push_back({x, byc[k + 1]});
             k += 2;

@@ -77,6 +77,7 @@ struct ta_server {
     std::mutex mu;                // running / start / stop
     bool running = false;
     std::atomic<uint32_t> active{0};
+    std::atomic<int> paused{0};   // > 0: calls are turned away (ta_server_pause)
     std::atomic<uint64_t> last_call{0};
     std::unique_ptr<std::atomic<uint32_t>[]> busy;
     std::thread keeper;
@@ -292,6 +293,11 @@ int ta_server_align(ta_server* s, const char* q, uint32_t n, const char* t, uint
     if (k == UINT32_MAX) return TA_ERR_UNSERVED;  // more concurrent callers than slots: the batch path
     hint = k;
     s->active.fetch_add(1);
+    if (s->paused.load() > 0) {  // (after counting itself: ta_server_pause waits for `active` to drain)
+        s->active.fetch_sub(1);
+        s->busy[k].store(0, std::memory_order_release);
+        return TA_ERR_UNSERVED;
+    }
     s->last_call.store(now_ns());
     {
         // (no hipEventQuery on this path: a HIP call per request costs microseconds;
@@ -363,6 +369,21 @@ int ta_server_last_times(const ta_server* s, uint32_t slot, double* us) {
     if (!s || !us || slot >= s->slots) return TA_ERR_ARG;
     const ta::ServeHdr* h = const_cast<ta_server*>(s)->hdr(slot);
     for (int k = 0; k < 4; ++k) us[k] = h->pad1[k] * 0.01;  // 100 MHz ticks
+    return TA_OK;
+}
+
+int ta_server_pause(ta_server* s) {
+    if (!s) return TA_ERR_ARG;
+    s->paused.fetch_add(1);
+    while (s->active.load() != 0) std::this_thread::yield();  // calls in flight finish (bounded by their pairs)
+    std::lock_guard<std::mutex> lk(s->mu);
+    s->stop_locked();
+    return TA_OK;
+}
+
+int ta_server_resume(ta_server* s) {
+    if (!s) return TA_ERR_ARG;
+    s->paused.fetch_sub(1);
     return TA_OK;
 }
 

@@ -120,17 +120,38 @@ bool server_enabled() {
     return on;
 }
 
+std::mutex g_srv_mu;
+std::map<std::pair<int, int>, ta_server*> g_servers;  // nullptr: creation failed, do not retry
+
 ta_server* server_for(int device, int type) {
-    static std::mutex mu;
-    static std::map<std::pair<int, int>, ta_server*> servers;  // nullptr: creation failed, do not retry
-    std::lock_guard<std::mutex> g(mu);
-    auto it = servers.find({device, type});
-    if (it != servers.end()) return it->second;
+    std::lock_guard<std::mutex> g(g_srv_mu);
+    auto it = g_servers.find({device, type});
+    if (it != g_servers.end()) return it->second;
     ta_server* s = nullptr;
     if (ta_server_create(device, type, kServerSlots, &s) != TA_OK) s = nullptr;
-    servers[{device, type}] = s;
+    g_servers[{device, type}] = s;
     return s;
 }
+
+// A batch's streams may share a hardware queue with a server's persistent
+// kernel (GPU_MAX_HW_QUEUES: 4 per process), and a kernel queued behind it
+// would wait until the server stops.  A batch therefore pauses the device's
+// servers around its launches (calls meanwhile take the batch path; the
+// server restarts with the next call after the batch).
+struct ServersPaused {
+    std::vector<ta_server*> s;
+    explicit ServersPaused(int device) {
+        {
+            std::lock_guard<std::mutex> g(g_srv_mu);
+            for (auto& kv : g_servers)
+                if (kv.first.first == device && kv.second) s.push_back(kv.second);
+        }
+        for (ta_server* x : s) (void)ta_server_pause(x);
+    }
+    ~ServersPaused() {
+        for (ta_server* x : s) (void)ta_server_resume(x);
+    }
+};
 
 // One batch at a time.  A new leader first waits (at most kGather) until as
 // many pairs are queued as its predecessor's batch held: the callers that
@@ -180,6 +201,7 @@ void run_batch_once(Request* const* reqs, size_t n, int& status) {
     std::string err;
     try {
         ta_context* ctx = thread_context(reqs[0]->device);
+        const ServersPaused paused(reqs[0]->device);
         // (the default plan also for small batches: packed couples and the lane
         // walk beat one int32 wave per pair with its walk inside the fill from 2
         // pairs up, 200x200: 8 pairs 221 vs 267 us, scripts/exp/batch_latency.py)

@@ -89,6 +89,13 @@ int ta_server_align(ta_server* server, const char* query, uint32_t query_len, co
                     uint32_t* target_begin, char* cigar, uint64_t cigar_capacity, uint32_t* cigar_len);
 /* 1 while the server's kernel is resident. */
 int ta_server_running(const ta_server* server);
+/* Pause / resume (counted).  While paused, ta_server_align returns
+ * TA_ERR_UNSERVED at once; ta_server_pause waits for the calls in flight and
+ * stops the kernel, so that work on other streams of the device never queues
+ * behind the persistent kernel on a shared hardware queue (a batch on the same
+ * device pauses the server around its launches). */
+int ta_server_pause(ta_server* server);
+int ta_server_resume(ta_server* server);
 /* Diagnostics: the device-side phase times (microseconds) of the last request
  * served in `slot`: [0] request + bytes into HBM, [1] fill + walk, [2] results
  * and CIGAR into the slot, [3] the system-scope release fence. */

@@ -8,6 +8,9 @@ for spec in "$@"; do
   kind="${spec%%:*}"
   case "$kind" in
     ubench)
+      # built on the box from its source (the binary is git- and gpurun-ignored)
+      /opt/rocm/bin/hipcc -O3 --offload-arch=gfx950 scripts/exp/ubench/valu_rates.hip -o scripts/exp/ubench/valu_rates \
+        || { echo "ubench build failed"; exit 1; }
       timeout -k 10 180 ./scripts/exp/ubench/valu_rates > gpurun_out/valu_rates.txt 2>&1 || { echo "ubench failed"; exit 1; }
       echo "ubench ok" ;;
     pytest)

@@ -195,7 +195,9 @@ void check_linear(const ta::Plan& pl, uint64_t budget) {
     for (size_t k = 0; k + 1 < pl.duals.size(); k += 2) {
         CHECK(pl.qlen[pl.duals[k]] == pl.qlen[pl.duals[k + 1]]);
         CHECK(pl.tlen[pl.duals[k]] == pl.tlen[pl.duals[k + 1]]);
+        CHECK(ta::n_passes(pl.qlen[pl.duals[k]]) < 64);  // hand-off tags epoch * 64 + pass + 1 (ta_dual.hip)
     }
+    for (size_t k = 0; k + 1 < pl.flexes.size(); k += 2) CHECK(ta::n_passes(pl.qlen[pl.flexes[k]]) < 64);
     uint64_t so = 0;
     for (uint32_t p = 0; p < P; ++p) {
         CHECK(pl.slot_off[p] == so);
@@ -217,6 +219,7 @@ void check_affine(const ta::AffinePlan& pl) {
         CHECK(c.ptr_entries <= pl.ws_ptr_entries);
     }
     CHECK(count == P);
+    for (size_t k = 0; k + 1 < pl.duals.size(); k += 2) CHECK(ta::n_passes(pl.qlen[pl.duals[k]]) < 64);
     bool piped = false;
     for (const auto& c : pl.chunks) piped |= c.spasses > 1;
     CHECK(piped == !pl.single_task_off.empty());
@@ -245,19 +248,22 @@ void check_affine(const ta::AffinePlan& pl) {
 void plan_worker(uint64_t seed, int iters) {
     uint64_t s = seed;
     for (int it = 0; it < iters; ++it) {
-        const uint32_t P = (uint32_t)(splitmix(s) % 300);
-        const int kind = (int)(splitmix(s) % 4);
+        const int kind = (int)(splitmix(s) % 5);
+        const uint32_t P = kind == 4 ? 2 + (uint32_t)(splitmix(s) % 3) : (uint32_t)(splitmix(s) % 300);
         std::vector<uint32_t> q(P), t(P);
         for (uint32_t p = 0; p < P; ++p) {
             switch (kind) {
                 case 0: q[p] = t[p] = 1000; break;                                                 // config 2
                 case 1: q[p] = (uint32_t)(splitmix(s) % 3000); t[p] = (uint32_t)(splitmix(s) % 3000); break;  // ragged
                 case 2: q[p] = 1 + (uint32_t)(splitmix(s) % 20000); t[p] = q[p] + (uint32_t)(splitmix(s) % 500); break;
-                default: q[p] = (uint32_t)(splitmix(s) % 4) * 1024 + 7; t[p] = 300 + (uint32_t)(splitmix(s) % 3); break;
+                case 3: q[p] = (uint32_t)(splitmix(s) % 4) * 1024 + 7; t[p] = 300 + (uint32_t)(splitmix(s) % 3); break;
+                default: q[p] = 63 * 1024 + 1 + (uint32_t)(splitmix(s) % 3) * 1024; t[p] = 40; break;  // 63..65 passes
             }
         }
         const int type = (int)(splitmix(s) % 3);
-        const int ma = 1 + (int)(splitmix(s) % 3), mi = -(int)(splitmix(s) % 3), g = -(int)(splitmix(s) % 3);
+        // (kind 4: all-zero scoring, whose values fit int16 at any length: only the pass bound stops couples)
+        const int ma = kind == 4 ? 0 : 1 + (int)(splitmix(s) % 3), mi = kind == 4 ? 0 : -(int)(splitmix(s) % 3),
+                  g = kind == 4 ? 0 : -(int)(splitmix(s) % 3);
         const uint64_t budget = (splitmix(s) & 1) ? (1ull << 40) : 4096ull + splitmix(s) % (64ull << 20);
         const uint32_t flags = (uint32_t)(splitmix(s) % 8) | ((splitmix(s) & 1) ? 32u : 0u) | ((splitmix(s) & 1) ? 64u : 0u);
         const bool cig = splitmix(s) % 4 != 0;

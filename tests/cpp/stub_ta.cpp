@@ -4,7 +4,9 @@
 // the shim (tests/test_host_sanitizers.py): the shim's per-thread contexts
 // and buffers are exercised from many threads without a GPU.  Never part of
 // the product (which has no CPU path).
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <string>
 
 #include "team_align_c.h"
@@ -46,6 +48,7 @@ int ta_device_count(void) { return 1; }
 // (the others take the shim's batch path, so both run under TSan).
 struct ta_server {
     int type = 0;
+    std::atomic<int> active{0}, paused{0};  // the pause protocol of ta_server.cpp
 };
 
 int ta_server_create(int device, int type, uint32_t slots, ta_server** out) {
@@ -65,9 +68,29 @@ int ta_server_fits(const ta_server* s, uint32_t n, uint32_t m, int match, int mi
 
 int ta_server_running(const ta_server* s) { return s != nullptr; }
 
+int ta_server_pause(ta_server* s) {
+    s->paused.fetch_add(1);
+    while (s->active.load() != 0) std::this_thread::yield();
+    return TA_OK;
+}
+
+int ta_server_resume(ta_server* s) {
+    s->paused.fetch_sub(1);
+    return TA_OK;
+}
+
 int ta_server_align(ta_server* s, const char* q, uint32_t n, const char* t, uint32_t m, int match, int mismatch,
                     int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* cigar, uint64_t cigar_cap,
                     uint32_t* cigar_len) {
+    s->active.fetch_add(1);
+    if (s->paused.load() > 0) {
+        s->active.fetch_sub(1);
+        return TA_ERR_UNSERVED;
+    }
+    struct Leave {
+        std::atomic<int>& a;
+        ~Leave() { a.fetch_sub(1); }
+    } leave{s->active};
     int sc = 0;
     unsigned b = 0;
     size_t cl = 0;

@@ -131,3 +131,39 @@ def test_reference_header_and_minimizers_link_against_library():
     assert "libteam_alignment.so" in dyn        # ... but bound to our library
     defined = subprocess.check_output(["nm", "-D", "--defined-only", A.LIB_PATH], text=True)
     assert A.TEAM_ALIGN_SYMBOL in defined
+
+
+@pytest.mark.skipif(not os.path.isfile(os.path.join(REF, "team_mapper.cpp")),
+                    reason="reference sources absent (GPU box)")
+def test_reference_team_mapper_cpp_links_unchanged():
+    """The reference's own team_mapper.cpp -- compiled in place, unmodified,
+    with the reference's team_minimizers.cpp (CMakeLists.txt:12-20, 32-36) --
+    links against libteam_alignment.so with nothing undefined, and its
+    team::Align calls (:666-678, :755-767) bind to our library at load time.
+    bioparser (:13-14) is an un-vendored submodule absent here: a TEST-ONLY
+    surface header (tests/cpp/bioparser_surface, the Parser/Create/Parse
+    declarations the file uses) lets it compile; it parses nothing, so this
+    proves the link only and pins no results.  (The file's quoted includes of
+    team_alignment.hpp / team_minimizers.hpp resolve next to it, to the
+    reference's own headers; ours is declaration-identical, see
+    test_team_align_symbol_matches_reference_header.)"""
+    out = os.path.join(ROOT, "build", "tm_link")
+    os.makedirs(out, exist_ok=True)
+    exe = os.path.join(out, "team_mapper")
+    libdir = os.path.dirname(A.LIB_PATH)
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-fopenmp", "-w",
+                           "-I", os.path.join(ROOT, "tests", "cpp", "bioparser_surface"),
+                           "-I", os.path.join(ROOT, "include"),
+                           os.path.join(REF, "team_mapper.cpp"),
+                           os.path.join(REF, "team_minimizers", "team_minimizers.cpp"),
+                           "-L", libdir, "-lteam_alignment", "-Wl,-rpath," + libdir, "-Wl,--no-undefined",
+                           "-o", exe])
+    und = subprocess.check_output(["nm", "-u", exe], text=True)
+    assert A.TEAM_ALIGN_SYMBOL in und                      # called, not defined, by the mapper
+    assert "libteam_alignment.so" in subprocess.check_output(["readelf", "-d", exe], text=True)
+    # every symbol bound at load time (LD_BIND_NOW): team::Align from our library
+    env = dict(os.environ, LD_BIND_NOW="1", LD_DEBUG="bindings")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 1 and "Not enough arguments" in r.stdout + r.stderr  # the mapper's own usage path
+    binds = [ln for ln in r.stderr.splitlines() if A.TEAM_ALIGN_SYMBOL in ln and "binding file" in ln]
+    assert binds and all(A.LIB_PATH in ln or "libteam_alignment.so" in ln for ln in binds), binds

@@ -1,9 +1,13 @@
 """bench.py's multi-rank result gather on CPU: world-size 2,
-3 and 4 gloo groups run bench.ResultGather over several steps of stand-in
+3, 4 and 8 gloo groups run bench.ResultGather over several steps of stand-in
 plans (host tensors, ragged per-rank pair counts and CIGAR sizes, one rank
 with no pairs); rank 0's gathered records and CIGAR bytes must be the
 rank-ordered concatenation of what every rank produced in the last step, and
 the other ranks must receive nothing (a gather to rank 0, not an all-gather).
+At 8 ranks config 4's path is rehearsed end to end: one ragged read set
+range-split by cells (shard.range_split), every rank aligning its slice (the
+CPU checker standing in for its GPU) into records padded to bench.py's P_max,
+and rank 0's gathered batch equal to the 1-rank result.
 The GPU run of the same path (bench.py --gpus 2, 2 ranks on one device) is
 tests/test_bench_gpu.py."""
 import os
@@ -83,10 +87,10 @@ def _worker(rank, world, port, q, max_len=40):
     dist.destroy_process_group()
 
 
-SIZES = [7, 3, 11, 0]
+SIZES = [7, 3, 11, 0, 5, 13, 1, 9]  # ragged per-rank pair counts, one rank empty
 
 
-@pytest.mark.parametrize("world,max_len", [(2, 40), (3, 40), (4, 40), (2, 400000)])
+@pytest.mark.parametrize("world,max_len", [(2, 40), (3, 40), (4, 40), (8, 40), (8, 30000), (2, 400000)])
 def test_result_gather_rank_order(world, max_len):
     """max_len 400000: MB-sized CIGAR byte transfers per rank and step (a config-4
     slice), which once stalled gloo when left in flight under the next gather."""
@@ -120,3 +124,78 @@ def test_bench_refuses_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 3 and "WORLD_SIZE=1 but --gpus 2" in r.stderr
+
+
+class _OraclePlan:
+    """A rank's slice of a read set aligned by the CPU checker, shaped like the
+    DevicePlan fields ResultGather reads."""
+
+    def __init__(self, part):
+        from oracle.pyoracle import Oracle
+
+        r = Oracle().align_batch(part, 2, 1, -1, -1, True, n_threads=1)
+        self.P = part.n_pairs
+        self.score = torch.from_numpy(r.scores.astype(np.int32))
+        self.target_begin = torch.from_numpy(r.target_begins.view(np.int32).copy())
+        self.cigar_len = torch.from_numpy(r.cigar_lens.view(np.int32).copy())
+        self.cig = [r.cigar(p) for p in range(part.n_pairs)]
+
+    compact_cigars = _FakePlan.compact_cigars
+
+
+def _cfg4_batch():
+    from bioinfo1_amd import synth
+
+    return synth.ragged_batch(90, 0, 400, seed=0xC4, alphabet=b"ACGTN")
+
+
+def _cfg4_worker(rank, world, port, q):
+    import torch.distributed as dist
+
+    import bench
+    from bioinfo1_amd import shard
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    full = _cfg4_batch()
+    cells = full.qlen.astype(np.int64) * full.tlen.astype(np.int64)
+    split = shard.range_split(cells, world)
+    lo, hi = split[rank]
+    P_max = max(h - l for l, h in split)  # bench.py's config-4 padding (run_workload)
+    g = bench.ResultGather(_FakeDist(dist, world, rank), P_max, True)
+    plan = _OraclePlan(full.slice(lo, hi))
+    for _ in range(2):  # two steps, as the timed loop posts them
+        g.post(plan)
+        g.clear_old()
+    g.drain()
+    if rank == 0:
+        sc, tb, cl, cig = g.last()
+        q.put(("root", sc.tolist(), tb.tolist(), cl.tolist(), cig, [h - l for l, h in split]))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_cfg4_range_split_gather_8_ranks():
+    """Config 4 at 8 ranks: uneven cell-balanced ranges (P_max padding of the
+    records), gathered to rank 0 in read order, equal to the 1-rank result."""
+    from oracle.pyoracle import Oracle
+
+    world = 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_cfg4_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    got = q.get(timeout=300)
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    sizes = got[5]
+    assert len(set(sizes)) > 1  # the ranges are uneven: records are padded to P_max
+    full = _cfg4_batch()
+    r = Oracle().align_batch(full, 2, 1, -1, -1, True)
+    assert got[1] == r.scores.tolist()
+    assert got[2] == r.target_begins.tolist()
+    assert got[3] == r.cigar_lens.tolist()
+    assert got[4] == b"".join(r.cigar(p) for p in range(full.n_pairs))

@@ -215,6 +215,34 @@ def test_team_align_dropin(kat_cases, random_cases):
         assert out == want
 
 
+def test_team_align_dropin_mixed_sizes(oracle):
+    """16 caller threads mixing pairs the resident server takes with pairs
+    past its limits (query > 4,096: the batch path).  A batch pauses the
+    device's servers around its launches, so no batch kernel queues behind
+    the persistent kernel on a shared hardware queue; every call finishes,
+    bounded in time, with the oracle's answers (shim stream /
+    queue sharing)."""
+    import time
+
+    exe = _shim_binary()
+    small = synth.ragged_batch(96, 1, 400, seed=0x31)
+    big = synth.related_batch(6, 4400, 600, seed=0x32)  # n > kSrvQMax: never served
+    pairs = [(small.query(p), small.target(p)) for p in range(small.n_pairs)]
+    at = [3 + 16 * k for k in range(big.n_pairs)]  # spread over the threads' strides
+    for k, p in enumerate(at):
+        pairs.insert(p, (big.query(k), big.target(k)))
+    b = synth.from_pairs(pairs)
+    want = oracle.align_batch(b, 1, 1, -1, -1, True)
+    lines = [f"1 1 -1 -1 {q.hex() or '-'} {t.hex() or '-'}" for q, t in pairs]
+    exp = [f"{int(want.scores[p])} {int(want.target_begins[p])} {want.cigar(p).hex() or '-'}"
+           for p in range(b.n_pairs)]
+    t0 = time.time()
+    out = subprocess.run([exe, "threads", "16"], input="\n".join(lines) + "\n", capture_output=True, text=True,
+                         timeout=120, check=True).stdout.splitlines()
+    assert out == exp
+    assert time.time() - t0 < 60
+
+
 def _check_full(aligner, batch, mode, sc):
     from oracle.pyoracle import cigar_check_batch
 

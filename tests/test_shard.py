@@ -61,7 +61,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 8])
 def test_gloo_gather_matches_single_process(world):
     from oracle.pyoracle import Oracle
 
