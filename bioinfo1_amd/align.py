@@ -29,7 +29,7 @@ LIB_PATH = os.path.join(HERE, "libteam_alignment.so")
 TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY, TA_ERR_RANGE, TA_ERR_UNSERVED = range(8)
 # ta_plan_create flags (include/team_align_c.h): kernel selection, same results
 TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2 = 1, 2, 4, 8, 16
-TA_PLAN_SERIAL_PASSES, TA_PLAN_PASS_MAJOR = 32, 64
+TA_PLAN_SERIAL_PASSES, TA_PLAN_PASS_MAJOR, TA_PLAN_NO_BLK = 32, 64, 128
 
 
 class AlignmentType(enum.IntEnum):
@@ -94,6 +94,7 @@ def lib() -> C.CDLL:
     L.ta_plan_flex_pairs.restype = C.c_uint32
     L.ta_plan_flex_pairs.argtypes = [C.c_void_p]
     L.ta_plan_fused.argtypes = [C.c_void_p]
+    L.ta_plan_walk.argtypes = [C.c_void_p]
     L.ta_plan_pair_chunks.argtypes = [C.c_void_p, u32p]
     L.ta_affine_plan_pair_chunks.argtypes = [C.c_void_p, u32p]
     L.ta_plan_execute.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
@@ -140,7 +141,7 @@ ABI_SYMBOLS = [
     "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_context_release",
     "ta_context_held_bytes", "ta_set_default_device", "ta_current_device", "ta_device_count",
     "ta_cigar_slot_bytes", "ta_align_batch", "ta_align_batch_flags", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes",
-    "ta_plan_workspace_bytes", "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_fused",
+    "ta_plan_workspace_bytes", "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_fused", "ta_plan_walk",
     "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_pair_chunks", "ta_affine_plan_pair_chunks", "ta_plan_execute_traceback", "ta_compact_cigars",
     "ta_affine_plan_create", "ta_affine_plan_destroy", "ta_affine_plan_cigar_slots_bytes",
     "ta_affine_plan_workspace_bytes", "ta_affine_plan_chunks", "ta_affine_plan_dual_pairs", "ta_affine_plan_execute", "ta_affine_plan_execute_fill",
@@ -427,6 +428,8 @@ class DevicePlan:
         self.dual_pairs = int(L.ta_affine_plan_dual_pairs(h)) if self.affine else int(L.ta_plan_dual_pairs(h))
         self.flex_pairs = 0 if self.affine else int(L.ta_plan_flex_pairs(h))
         self.fused = False if self.affine else bool(L.ta_plan_fused(h))
+        w = -1 if self.affine else int(L.ta_plan_walk(h))
+        self.walk, self.blk = (w & 0xFF, bool(w & 0x100)) if w >= 0 else (None, False)
         self.aligner = aligner
 
     def _stream(self):

@@ -38,6 +38,7 @@ struct ta_plan {
     uint32_t* d_stask_off = nullptr;  // pipelined int32 fill: per single, its first task
     uint64_t* d_stasks = nullptr;     // ... its tasks in ticket order
     void* d_spout = nullptr;          // ... PassOut per task
+    uint8_t* d_pflag = nullptr;       // blk plans: per pair, handed back by the dual fill (band walk skips it)
 };
 
 namespace {
@@ -50,7 +51,7 @@ bool valid_type(int t) { return t == TA_GLOBAL || t == TA_LOCAL || t == TA_SEMI_
 struct PlanOffs {
     uint64_t qlen, tlen, order, singles, duals, flexes, task_off, tasks, stask_off, stasks, ptr_off, bnd_off, slot_off,
         err, tickets;
-    uint64_t goal_i, goal_j, fb, pout, dpout, spout;
+    uint64_t goal_i, goal_j, fb, pout, dpout, spout, pflag;
 };
 
 // PassOut[2] (24 bytes each) per (pass, couple) of the largest multi-pass dual chunk
@@ -93,6 +94,7 @@ void layout_scratch(const ta::Plan& h, ta::BlockLayout& L, PlanOffs& o) {
     o.pout = L.add(h.flexes.empty() ? 0 : h.flex_task_off.back() * 48ull + 16);
     o.dpout = L.add(dual_pout_bytes(h));
     o.spout = L.add(h.single_tasks.size() * 24ull);
+    o.pflag = L.add(h.blk ? h.n_pairs : 0);
 }
 
 void pack(const ta::Plan& h, const PlanOffs& o, uint8_t* base) {
@@ -140,6 +142,7 @@ void bind(ta_plan* pl, uint8_t* d, const PlanOffs& o) {
     pl->d_stask_off = u32(o.stask_off);
     pl->d_stasks = u64(o.stasks);
     pl->d_spout = d + o.spout;
+    pl->d_pflag = d + o.pflag;
 }
 
 int check_args(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type) {
@@ -160,6 +163,8 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         if (int r = ta_host::grow(ctx, ctx->ws_ptrs, h.ws_ptr_dwords * 4ull)) return r;
     if (h.ws_bnd_words)
         if (int r = ta_host::grow(ctx, ctx->ws_bnd, h.ws_bnd_words * 4ull)) return r;
+    if (h.walk_group == 64 && h.want_cigar)
+        if (int r = ta_host::grow(ctx, ctx->ws_runs, 2 * h.slots_bytes + 64)) return r;
     uint32_t* d_ptrs = static_cast<uint32_t*>(ctx->ws_ptrs.p);
     int32_t* d_bnd = static_cast<int32_t*>(ctx->ws_bnd.p);
     if (fill) {
@@ -196,6 +201,8 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         a.slot_off = pl->d_slot_off;
         a.cigar_start = io->cigar_start;
         a.cigar_len = io->cigar_len;
+        a.blk = h.blk ? 1u : 0u;
+        a.pflag = (h.blk && h.walk_group == 64) ? pl->d_pflag : nullptr;
         if (ch.scount) {  // launched first: it may run on the aux stream beside the packed fill
             ta::FillArgs a1 = a;
             a1.order = pl->d_singles;
@@ -306,7 +313,23 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         t.match = h.match;
         t.mismatch = h.mismatch;
         t.gap = h.gap;
-        TA_HIP(ctx, ta::launch_traceback(h.type, t, s, h.walk_group));
+        t.blk = h.blk ? 1u : 0u;
+        if (h.walk_group == 64) {
+            // band walks (one lane per pair), then the pairs of the couples the dual
+            // fill handed back ('-' bytes) in the one-pair walk: its list and count
+            t.pflag = pl->d_pflag;
+            t.runs = static_cast<uint32_t*>(ctx->ws_runs.p);
+            TA_HIP(ctx, ta::launch_traceback(h.type, t, s, 64));
+            ta::TraceArgs f = t;
+            f.order = pl->d_fb + 2ull * ch.cbegin;
+            f.begin = 0;
+            f.count = 2 * (ch.dcount + ch.fcount);
+            f.count_dev = pl->d_fb + h.n_dual_pairs + c;
+            f.pflag = nullptr;
+            TA_HIP(ctx, ta::launch_traceback(h.type, f, s, 0));
+        } else {
+            TA_HIP(ctx, ta::launch_traceback(h.type, t, s, h.walk_group));
+        }
         roctxRangePop();
     }
     return TA_OK;
@@ -402,7 +425,7 @@ void ta_context_release(ta_context* ctx) {
     std::lock_guard<std::mutex> lock(ctx->mu);
     (void)hipSetDevice(ctx->device);
     if (ctx->used) (void)hipEventSynchronize(ctx->ev_last);
-    for (auto* b : {&ctx->blk, &ctx->out, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd}) ta_host::release(*b, false);
+    for (auto* b : {&ctx->blk, &ctx->out, &ctx->dst, &ctx->ws_ptrs, &ctx->ws_bnd, &ctx->ws_runs}) ta_host::release(*b, false);
     for (auto* b : {&ctx->pin_in, &ctx->pin_out}) ta_host::release(*b, true);
 }
 
@@ -421,7 +444,7 @@ uint64_t ta_context_held_bytes(const ta_context* ctx) {
     uint64_t n = 0;
     // only what a plan's workspace can reuse: the code and pass-boundary buffers
     // (staging and output buffers are not handed to a plan's chunks)
-    for (const auto* b : {&ctx->ws_ptrs, &ctx->ws_bnd}) n += b->cap;
+    for (const auto* b : {&ctx->ws_ptrs, &ctx->ws_bnd, &ctx->ws_runs}) n += b->cap;
     return n;
 }
 
@@ -480,6 +503,11 @@ uint32_t ta_plan_chunks(const ta_plan* pl) { return pl ? (uint32_t)pl->h.chunks.
 uint32_t ta_plan_dual_pairs(const ta_plan* pl) { return pl ? pl->h.n_dual_pairs : 0; }
 uint32_t ta_plan_flex_pairs(const ta_plan* pl) { return pl ? (uint32_t)pl->h.flexes.size() : 0; }
 int ta_plan_fused(const ta_plan* pl) { return pl && pl->h.fused ? 1 : 0; }
+
+int ta_plan_walk(const ta_plan* pl) {
+    if (!pl) return -1;
+    return pl->h.walk_group | (pl->h.blk ? 0x100 : 0);
+}
 
 int ta_plan_pair_chunks(const ta_plan* pl, uint32_t* chunk_of_pair) {
     if (!pl || !chunk_of_pair) return TA_ERR_ARG;

@@ -42,6 +42,9 @@ struct ta_context {
     // Traceback-code and pass-boundary workspace, shared by every plan of this
     // context and grown at execute time (a plan's chunks are sized by its budget).
     Buf ws_ptrs, ws_bnd;
+    // Band walks (ta_walk_band.h): the run words of every pair before they are
+    // formatted into its CIGAR slot (2 x the plan's slot bytes).
+    Buf ws_runs;
     uint32_t cu_count = 256;
     uint32_t epoch = 0;  // flexible-fill launches so far (tags of their pass hand-off records)
 };

@@ -182,7 +182,7 @@ __device__ __forceinline__ uint32_t seq_window(const uint8_t* S, uint32_t base, 
 template <int MODE>
 __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, uint32_t m, uint32_t gi, uint32_t gj,
                                                char* slot, uint64_t cap, int lane, uint64_t* start_in_slot,
-                                               uint32_t* len, const WalkSeq& seq) {
+                                               uint32_t* len, const WalkSeq& seq, bool blk = false) {
     RunWriter w{slot + cap, 0u, 0u, 0u, 0u, 0u, 0u, lane};
     int H = seq.h;  // local: cost of the walk's current cell
     uint32_t qbase = 0, tbase = 0, qw = 0, tw = 0;  // local: byte windows (seq_window)
@@ -246,7 +246,13 @@ __device__ __forceinline__ void traceback_pair(const uint32_t* P, uint32_t n, ui
             tt0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)(max(t, 63u) - 63u));
             const uint32_t ts = tt0 + (uint32_t)lane;
             c0 = c1 = c2 = c3 = 0;
-            if (ts < Tmax) {
+            if (ts < Tmax && blk) {  // blocked layout: 4 stripes of one step, 64 bytes apart
+                const uint32_t* q = P + blk_index(tP, ts, tL0, blk_count(m));
+                c0 = q[0];
+                c1 = q[kBlkSteps];
+                c2 = q[2 * kBlkSteps];
+                c3 = q[3 * kBlkSteps];
+            } else if (ts < Tmax) {
                 const uint32_t* q = P + ((uint64_t)tP * Tmax + ts) * kWave + tL0;
                 c0 = q[0];
                 c1 = q[1];

@@ -48,6 +48,9 @@ struct DualIo {
     const uint64_t* rec_r;
     uint32_t tag_w, tag_r;
     uint32_t* err;
+    // blocked layout (BLK): this wave's LDS staging of 16 steps, [pair][step][lane]
+    uint32_t* cbuf;
+    uint32_t nb;  // blk_count(m)
 };
 
 typedef __attribute__((address_space(1))) unsigned long long gu64d;
@@ -80,7 +83,10 @@ __device__ __forceinline__ int dual_poll_chunk(const DualIo& io, uint32_t m, uin
 // a tree of three-input maxima (v_pk_maximum3_f16 on non-negative int16).
 // CLS: both queries hold only A, C, G, T -- mismatch flags by table lookup
 // (ta_packed.h mismatch_table / row_selector), one v_perm per row.
-template <int MODE, bool CIGAR, int NV, bool M3, bool CLS>
+// BLK: codes in the blocked layout (ta_layout.h blk_index): each step's two
+// dwords go to this wave's LDS staging, and every 16 steps each lane writes its
+// stripe's 16 steps of both pairs as 64 contiguous bytes (4 x 16-byte stores).
+template <int MODE, bool CIGAR, int NV, bool M3, bool CLS, bool BLK = false>
 __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
                                              uint32_t pass, bool last_pass, int lane, int off = 0) {
     constexpr int R = kRows;
@@ -155,8 +161,28 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     };
     int bcur = top_chunk(0), bnext = top_chunk(1);
     const uint32_t steps = m + nl - 1;
-    uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * Tmax * kWave : nullptr;
-    uint32_t* prow1 = CIGAR ? io.ptrs[1] + (uint64_t)pass * Tmax * kWave : nullptr;
+    uint32_t* prow0 = CIGAR ? io.ptrs[0] + (BLK ? (uint64_t)pass * io.nb * (kBlkSteps * kWave) : (uint64_t)pass * Tmax * kWave) : nullptr;
+    uint32_t* prow1 = CIGAR ? io.ptrs[1] + (BLK ? (uint64_t)pass * io.nb * (kBlkSteps * kWave) : (uint64_t)pass * Tmax * kWave) : nullptr;
+    // BLK: the staged 16 steps of block b -> [b][lane][16] of both pairs
+    auto blk_flush = [&](uint32_t b) {
+        const uint64_t at = ((uint64_t)b * kWave + (uint32_t)lane) * kBlkSteps;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            uint32_t* dst = (h ? prow1 : prow0) + at;
+            const uint32_t* src = io.cbuf + h * (kBlkSteps * kWave) + lane;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                // (one 16-byte piece at a time: the step loop's registers are all live here)
+                __builtin_amdgcn_sched_barrier(0);
+                uint4 v;
+                v.x = src[(4 * q + 0) * kWave];
+                v.y = src[(4 * q + 1) * kWave];
+                v.z = src[(4 * q + 2) * kWave];
+                v.w = src[(4 * q + 3) * kWave];
+                *reinterpret_cast<uint4*>(dst + 4 * q) = v;
+            }
+        }
+    };
 
     // Chunk reloads (every 256 steps: target bytes; every 64: the row above)
     // are hoisted out of the step loop by run_steps.
@@ -284,10 +310,19 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         }
         if (CIGAR) {
             // per pair: [I rows 8-15, I rows 0-7, D rows 8-15, D rows 0-7] (ta_internal.h Code)
-            // 32-bit byte offset from the uniform row base (SGPR base + VGPR offset stores)
-            const uint32_t off = (t * kWave + (uint32_t)lane) * 4u;
-            *(uint32_t*)((char*)prow0 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
-            *(uint32_t*)((char*)prow1 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
+            const uint32_t cA = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
+            const uint32_t cB = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
+            if constexpr (BLK) {
+                const uint32_t sl = (t & 15u) * kWave + (uint32_t)lane;
+                io.cbuf[sl] = cA;
+                io.cbuf[kBlkSteps * kWave + sl] = cB;
+                if ((t & 15u) == 15u || t + 1 == steps) blk_flush(t >> 4);
+            } else {
+                // 32-bit byte offset from the uniform row base (SGPR base + VGPR offset stores)
+                const uint32_t off = (t * kWave + (uint32_t)lane) * 4u;
+                *(uint32_t*)((char*)prow0 + off) = cA;
+                *(uint32_t*)((char*)prow1 + off) = cB;
+            }
         }
     };
     const uint32_t ramp_end = min(nl - 1, steps);
@@ -361,7 +396,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     return out;
 }
 
-template <int MODE, bool CIGAR, bool CLS>
+template <int MODE, bool CIGAR, bool CLS, bool BLK = false>
 __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo& io, uint32_t n, uint32_t m,
                                                 uint32_t pass, bool last_pass, int lane) {
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
@@ -370,9 +405,9 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
         const int off = local_max3_offset(n, m, a.match, a.mismatch, a.gap);  // wave-uniform
         if (off >= 0) {
             if (nv == kRows)
-                return dual_pass<MODE, CIGAR, kRows, true, CLS>(a, io, n, m, pass, last_pass, lane, off);
+                return dual_pass<MODE, CIGAR, kRows, true, CLS, BLK>(a, io, n, m, pass, last_pass, lane, off);
 #define TA_NV_CASE(k) \
-    case k: return dual_pass<MODE, CIGAR, k, true, CLS>(a, io, n, m, pass, last_pass, lane, off);
+    case k: return dual_pass<MODE, CIGAR, k, true, CLS, BLK>(a, io, n, m, pass, last_pass, lane, off);
             switch (nv) {
                 TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
                 TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -382,9 +417,9 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
         }
     }
     if (MODE == kGlobal || nv == kRows)
-        return dual_pass<MODE, CIGAR, kRows, false, CLS>(a, io, n, m, pass, last_pass, lane);
+        return dual_pass<MODE, CIGAR, kRows, false, CLS, BLK>(a, io, n, m, pass, last_pass, lane);
 #define TA_NV_CASE(k) \
-    case k: return dual_pass<MODE, CIGAR, k, false, CLS>(a, io, n, m, pass, last_pass, lane);
+    case k: return dual_pass<MODE, CIGAR, k, false, CLS, BLK>(a, io, n, m, pass, last_pass, lane);
     switch (nv) {
         TA_NV_CASE(1) TA_NV_CASE(2) TA_NV_CASE(3) TA_NV_CASE(4) TA_NV_CASE(5) TA_NV_CASE(6) TA_NV_CASE(7)
         TA_NV_CASE(8) TA_NV_CASE(9) TA_NV_CASE(10) TA_NV_CASE(11) TA_NV_CASE(12) TA_NV_CASE(13) TA_NV_CASE(14)
@@ -409,9 +444,11 @@ constexpr uint32_t kDualSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to 
 // belongs to a wave that took an earlier ticket and is running;
 // each wave writes its pass's PassOut and dual_combine_kernel folds them.
 // Otherwise one wave per couple sweeps its passes.
-template <int MODE, bool CIGAR>
+template <int MODE, bool CIGAR, bool BLK = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
+    // BLK: 8 KB of code staging per wave (16 steps x 64 lanes x 2 pairs)
+    __shared__ uint32_t cbuf_all[BLK ? kWavesPerBlock * 2 * kBlkSteps * kWave : 1];
     uint32_t widx, p_only = 0;
     const bool pipe = a.ticket != nullptr;
     if (pipe) {
@@ -442,6 +479,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     io.rec_r = nullptr;
     io.tag_w = io.tag_r = 0;
     io.err = a.err;
+    io.cbuf = cbuf_all + (BLK ? (threadIdx.x >> 6) * (2 * kBlkSteps * kWave) : 0);
+    io.nb = blk_count(m);
     bool dash = false, qother = false;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -456,12 +495,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
         }
     }
     const bool cls = __ballot(qother) == 0;  // queries of A, C, G, T only: table mismatch flags
+    const bool any_dash = __ballot(dash) != 0;
+    if (a.pflag && lane == 0 && (!pipe || p_only == 0)) {  // blk plans: the band walk skips handed-back pairs
+        a.pflag[p[0]] = any_dash ? 1 : 0;
+        a.pflag[p[1]] = any_dash ? 1 : 0;
+    }
     // A '-' (a free gap step, team_alignment.cpp:25-28) changes the up gain per
     // row (query) or the left gain per step (target); those variants would cost
     // this kernel ~30 VGPRs and per-step selects for input real reads never
     // contain, so such couples go to the int32 fill (launched right after,
     // same workspace).
-    if (__ballot(dash)) {
+    if (any_dash) {
         if (lane == 0) {
             if (!pipe || p_only == 0) {
                 // a self-coupled pair (p[0] == p[1], ta_planner.cpp) is handed back once:
@@ -489,8 +533,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
         io.tag_w = a.epoch * 64u + p_only + 1u;
         io.tag_r = a.epoch * 64u + p_only;
         const bool last_pass = p_only + 1 == passes;
-        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, p_only, last_pass, lane)
-                              : dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, p_only, last_pass, lane);
+        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true, BLK>(a, io, n, m, p_only, last_pass, lane)
+                              : dual_pass_nv<MODE, CIGAR, false, BLK>(a, io, n, m, p_only, last_pass, lane);
         if (lane == 0) {
             po[0] = o.o[0];
             po[1] = o.o[1];
@@ -507,8 +551,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     }
     for (uint32_t pass = 0; pass < passes; ++pass) {
         const bool last_pass = pass + 1 == passes;
-        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true>(a, io, n, m, pass, last_pass, lane)
-                              : dual_pass_nv<MODE, CIGAR, false>(a, io, n, m, pass, last_pass, lane);
+        const DualOut o = cls ? dual_pass_nv<MODE, CIGAR, true, BLK>(a, io, n, m, pass, last_pass, lane)
+                              : dual_pass_nv<MODE, CIGAR, false, BLK>(a, io, n, m, pass, last_pass, lane);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             if (MODE != kGlobal && o.o[h].h > best_h[h]) {
@@ -596,11 +640,23 @@ __global__ void dual_combine_kernel(FillArgs a) {
 }  // namespace
 
 #ifdef TA_DUAL_MODE
+#ifdef TA_DUAL_BLK
+hipError_t launch_dual_blk(const FillArgs& a, hipStream_t s) {
+#else
 template <>
 hipError_t launch_dual_mode<TA_DUAL_MODE, (TA_DUAL_CIGAR != 0)>(const FillArgs& a, hipStream_t s) {
+#endif
     if (!a.count) return hipSuccess;
+#ifdef TA_DUAL_BLK  // (its own translation unit: the blocked-layout local fill)
+    hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, true, true>), dual_grid(a.ticket ? a.n_tasks : a.count),
+                       dim3(kBlock), 0, s, a);
+#else
+#if TA_DUAL_MODE == 1 && TA_DUAL_CIGAR
+    if (a.blk) return launch_dual_blk(a, s);
+#endif
     hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, TA_DUAL_CIGAR != 0>), dual_grid(a.ticket ? a.n_tasks : a.count),
                        dim3(kBlock), 0, s, a);
+#endif
     if (a.ticket)
         hipLaunchKernelGGL(dual_combine_kernel<TA_DUAL_MODE>, dim3((a.count + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();

@@ -64,6 +64,12 @@ struct FillArgs {
     // multi-pass dual chunks: ticket t = level t / count of couple t % count;
     // pass = level (pass-major) or level - (chunk passes - couple passes) (end-aligned)
     uint32_t end_aligned;
+    // blocked code layout (ta_layout.h blk_index): the dual fill stages 16 steps
+    // in LDS and writes [block][lane][16 steps]; the int32 fill stores per step
+    uint32_t blk;
+    // blk plans: per pair, 1 when its couple was handed back ('-' bytes; the
+    // band walk leaves it to the fallback walk), written by the dual fill
+    uint8_t* pflag;
 };
 
 struct TraceArgs {
@@ -86,6 +92,10 @@ struct TraceArgs {
     const uint8_t* tbytes;
     const uint64_t* toff;
     int match, mismatch, gap;
+    uint32_t blk;                // codes in the blocked layout (ta_layout.h blk_index)
+    const uint8_t* pflag;        // band walk: pairs to leave to the fallback walk (FillArgs.pflag)
+    const uint32_t* count_dev;   // non-null: pair count read on the device (the hand-back list)
+    uint32_t* runs;              // band walks: run words, pair p's at runs + slot_off[p] / 2 (format_runs_kernel)
 };
 
 struct CompactArgs {
@@ -141,12 +151,16 @@ struct ServeArgs {
 hipError_t launch_fill(int mode, bool cigar, bool wide, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_fill_mode(bool wide, const FillArgs& a, hipStream_t s);
-// group: 32 = local walks of two pairs per wave (ta_walk2.h), 0 = one pair per wave
+// group: 32 = local walks of two pairs per wave (ta_walk2.h), 16 = lane walks
+// (ta_walk_lane.h), 64 = band walks (one lane per pair, ta_walk_band.h; blocked
+// layout), 0 = one pair per wave
 hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int group);
 // Dual-pair packed int16 fill (ta_dual.hip): a.order holds 2 pair ids per wave.
 hipError_t launch_dual(int mode, bool cigar, const FillArgs& a, hipStream_t s);
 template <int MODE, bool CIGAR>
 hipError_t launch_dual_mode(const FillArgs& a, hipStream_t s);
+// the local CIGAR dual fill in the blocked code layout (ta_dual.hip, TA_DUAL_BLK)
+hipError_t launch_dual_blk(const FillArgs& a, hipStream_t s);
 // Flexible two-pair fill (ta_flex.hip, global / semi-global): a.order holds 2
 // pair ids per wave, the larger n first; both with the same pass count and
 // n mod 16; rebased int16 values, so any length fits.

@@ -29,6 +29,7 @@
 #include "ta_device.h"
 #include "ta_walk2.h"
 #include "ta_walk_lane.h"
+#include "ta_walk_band.h"
 
 namespace ta {
 namespace {
@@ -279,7 +280,13 @@ __device__ __forceinline__ PassOut run_pass(const FillArgs& a, const uint8_t* Q,
                     B.B[j] = H[R - 1];
             }
         }
-        if (CIGAR) prow[t * kWave + lane] = (accD << kDPlane) | accI;
+        if (CIGAR) {
+            const uint32_t code = (accD << kDPlane) | accI;
+            // (blocked layout: the couples a blk plan's dual fill hands back; one
+            // dword per lane 64 bytes apart, rare enough to need no staging)
+            if (a.blk) ptrs[blk_index(pass, t, (uint32_t)lane, blk_count(m))] = code;
+            else prow[t * kWave + lane] = code;
+        }
     };
     // lanes 0..nl-1 are all active for t in [nl-1, m-1]
     const uint32_t ramp_end = min(nl - 1, steps);
@@ -883,7 +890,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_TB_WP
     // Wave-strided over the pairs (one wave per pair: the grid covers them all).
     const int lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * kWavesPerBlock;
-    for (uint32_t widx = wave_id(); widx < a.count; widx += stride) {
+    const uint32_t count = a.count_dev ? *a.count_dev : a.count;  // (the band walk's fallback: the hand-back list)
+    for (uint32_t widx = wave_id(); widx < count; widx += stride) {
         const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
         const uint32_t n = a.qlen[p], m = a.tlen[p];
         uint64_t st;
@@ -891,7 +899,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_TB_WP
         const WalkSeq seq{a.qbytes + a.qoff[p], a.tbytes + a.toff[p], MODE == kLocal ? a.score[p] : 0, a.match,
                           a.mismatch, a.gap};
         traceback_pair<MODE>(a.ptrs + a.ptr_off[p], n, m, a.goal_i[p], a.goal_j[p], a.slots + a.slot_off[p],
-                             cigar_slot_bytes(n, m), lane, &st, &len, seq);
+                             cigar_slot_bytes(n, m), lane, &st, &len, seq, a.blk != 0);
         if (lane == 0) {
             a.cigar_start[p] = a.slot_off[p] + st;
             a.cigar_len[p] = len;
@@ -913,6 +921,20 @@ template <int G>
 __global__ __launch_bounds__(kWave) void traceback_lane_kernel(TraceArgs a) {
     __shared__ uint32_t lds[(64 / G) * kLwGroupDw];
     traceback_lane_local<G>(a, lds, (int)threadIdx.x);
+}
+
+// Local walks of blocked-layout plans, one lane per pair, 64 per one-wave
+// block (ta_walk_band.h).
+__global__ __launch_bounds__(kWave) void traceback_band_kernel(TraceArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kWave * kBwRegion];
+    traceback_band_local(a, lds, (int)threadIdx.x);
+}
+
+// ... and their runs into CIGAR text, one wave per pair.
+__global__ __launch_bounds__(kBlock) void format_runs_kernel(TraceArgs a) {
+    const uint32_t w = wave_id();
+    if (w >= a.count) return;
+    format_runs(a, a.order ? a.order[a.begin + w] : a.begin + w, threadIdx.x & 63);
 }
 
 __global__ __launch_bounds__(kBlock) void compact_kernel(CompactArgs a) {
@@ -1012,6 +1034,21 @@ hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int gro
         hipLaunchKernelGGL(traceback_group_kernel<32>, grid_for((a.count + 1) / 2), b, 0, s, a);
         return hipGetLastError();
     }
+    if (mode == kLocal && group == 64) {  // band walks (blocked layout), one lane per pair
+        hipLaunchKernelGGL(traceback_band_kernel, dim3((a.count + kWave - 1) / kWave), dim3(kWave), 0, s, a);
+        hipLaunchKernelGGL(format_runs_kernel, g, b, 0, s, a);
+        return hipGetLastError();
+    }
+    if (a.count_dev) {  // the band walk's fallback (the hand-back list, count on the device): capped grid
+        const dim3 gc((std::min<uint32_t>(a.count, 1024u) + kWavesPerBlock - 1) / kWavesPerBlock);
+        switch (mode) {
+            case kGlobal: hipLaunchKernelGGL(traceback_kernel<kGlobal>, gc, b, 0, s, a); break;
+            case kLocal: hipLaunchKernelGGL(traceback_kernel<kLocal>, gc, b, 0, s, a); break;
+            case kSemi: hipLaunchKernelGGL(traceback_kernel<kSemi>, gc, b, 0, s, a); break;
+            default: return hipErrorInvalidValue;
+        }
+        return hipGetLastError();
+    }
     if (mode == kLocal && group == 16) {  // lane walks (TA_LW_G lanes per pair)
         constexpr int W = 64 / TA_LW_G;
         hipLaunchKernelGGL(traceback_lane_kernel<TA_LW_G>, dim3((a.count + W - 1) / W), dim3(kWave), 0, s, a);
@@ -1032,6 +1069,17 @@ extern "C" int ta_lw_prof(unsigned long long* out, int reset) {
     if (reset) {
         unsigned long long z[8] = {};
         if (hipMemcpyToSymbol(HIP_SYMBOL(lw_prof), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#endif
+
+#ifdef TA_BW_PROF
+extern "C" int ta_bw_prof(unsigned long long* out, int reset) {
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(bw_prof), sizeof(unsigned long long) * 8) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[8] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(bw_prof), z, sizeof(z)) != hipSuccess) return -1;
     }
     return 0;
 }

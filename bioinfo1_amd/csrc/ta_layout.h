@@ -58,6 +58,23 @@ TA_HD inline uint32_t n_passes(uint32_t n) { return (n + kPassRows - 1) / kPassR
 TA_HD inline uint64_t ptr_dwords(uint32_t n, uint32_t m) {
     return (n == 0 || m == 0) ? 0 : (uint64_t)n_passes(n) * pass_steps(m) * kWave;
 }
+// Blocked code layout (plans with `blk`): per pass, blocks of 16
+// steps, [block][lane][16 steps] dwords -- the 16 consecutive steps of one
+// stripe (a 16 x 16 square of cells) are 64 contiguous bytes, the unit a walk
+// that follows a stripe reads, instead of 16 dwords 256 bytes apart in the
+// [step][lane] layout.
+constexpr int kBlkSteps = 16;
+TA_HD inline uint32_t blk_count(uint32_t m) { return (pass_steps(m) + kBlkSteps - 1) / kBlkSteps; }
+TA_HD inline uint64_t ptr_dwords_blk(uint32_t n, uint32_t m) {
+    return (n == 0 || m == 0) ? 0 : (uint64_t)n_passes(n) * blk_count(m) * kBlkSteps * kWave;
+}
+TA_HD inline uint64_t ptr_dwords_any(uint32_t n, uint32_t m, bool blk) {
+    return blk ? ptr_dwords_blk(n, m) : ptr_dwords(n, m);
+}
+// dword of (pass, step t, lane) in the blocked layout (nb = blk_count(m))
+TA_HD inline uint64_t blk_index(uint32_t pass, uint32_t t, uint32_t lane, uint32_t nb) {
+    return (((uint64_t)pass * nb + (t >> 4)) * kWave + lane) * kBlkSteps + (t & 15u);
+}
 // Pass-boundary row (int32 per column) needed only when the query spans > 1 pass.
 TA_HD inline uint64_t bnd_words(uint32_t n, uint32_t m) {
     return n_passes(n) > 1 ? (uint64_t)m + 1 + kWave : 0;

@@ -298,6 +298,17 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         for (uint32_t p : rest) units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
     }
     std::stable_sort(units.begin(), units.end(), [](const Unit& x, const Unit& y) { return x.cost > y.cost; });
+    // Local walks of short pairs in plans of equal-shape couples only run as band
+    // walks (one lane per pair, ta_walk_band.h) over the blocked code layout:
+    // the dual fill stages each stripe's 16 steps and writes them as 64
+    // contiguous bytes, the unit a walk following its stripe reads.
+    uint64_t len_sum = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) len_sum += (uint64_t)qlen[p] + tlen[p];
+    const bool short_pairs = len_sum <= 6000ull * std::max<uint32_t>(n_pairs, 1);
+    bool all_dual = !units.empty();
+    for (const Unit& u : units) all_dual = all_dual && u.kind == 1;
+    pl.blk = want_cigar && type == kLocal && all_dual && short_pairs && mag < (1ull << 22) &&
+             !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2));
     // Multi-pass int32 pairs run one wave per (pair, pass) like the packed
     // fills (their passes overlap instead of following each other on one
     // wave); the walk then runs in the traceback kernel.
@@ -305,7 +316,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     auto unit_codes = [&](size_t k) -> uint64_t {
         const Unit& u = units[k];
         if (!want_cigar) return 0;
-        return ptr_dwords(qlen[u.a], tlen[u.a]) + (u.kind && u.a != u.b ? ptr_dwords(qlen[u.b], tlen[u.b]) : 0);
+        return ptr_dwords_any(qlen[u.a], tlen[u.a], pl.blk) +
+               (u.kind && u.a != u.b ? ptr_dwords_any(qlen[u.b], tlen[u.b], pl.blk) : 0);
     };
     auto unit_waves = [&](size_t k) -> uint64_t {
         const Unit& u = units[k];
@@ -337,7 +349,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
             const uint32_t x = q[h];
             pl.ptr_off[x] = cur.ptr_dwords;
             pl.bnd_off[x] = cur.bnd_words;
-            const uint64_t xd = want_cigar ? ptr_dwords(qlen[x], tlen[x]) : 0;
+            const uint64_t xd = want_cigar ? ptr_dwords_any(qlen[x], tlen[x], pl.blk) : 0;
             // flex: pair A holds both pairs' absolute int32 boundary rows, interleaved;
             // each pair keeps a region of its own for the int32 fallback ('-' in a query)
             uint64_t bw = bnd_words(qlen[x], tlen[x]);
@@ -384,10 +396,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     // config 2; their runs are clipped to 32 cells, so batches of long pairs (long
     // M runs) keep the one-pair walk (config 3 local: 4.1 vs 6.3 ms).  24-bit
     // multiplies of the scores in the run walks.
-    uint64_t len_sum = 0;
-    for (uint32_t p = 0; p < n_pairs; ++p) len_sum += (uint64_t)qlen[p] + tlen[p];
-    const bool short_pairs = len_sum <= 6000ull * std::max<uint32_t>(n_pairs, 1);
-    if ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) pl.walk_group = 0;
+    if (pl.blk) pl.walk_group = gap <= 0 ? 64 : 0;  // (a positive gap lowers the cost in gap runs: one-pair walk)
+    else if ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) pl.walk_group = 0;
     else if ((flags & kPlanWalk2) || gap < -128 || gap > 127) pl.walk_group = 32;
     else pl.walk_group = 16;
     // (Each dual wave walking its own two pairs right after its fill measured

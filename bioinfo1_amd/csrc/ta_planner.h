@@ -22,6 +22,7 @@ constexpr uint32_t kPlanWalk1 = 8u;      // local walks: one pair per wave (trac
 constexpr uint32_t kPlanWalk2 = 16u;     // local walks: two pairs per wave (ta_walk2.h), not lane walks
 constexpr uint32_t kPlanSerialPasses = 32u;  // int32 fill: one wave sweeps all of a pair's passes
 constexpr uint32_t kPlanPassMajor = 64u;     // pass tasks ticketed start-aligned (every pass 0 first)
+constexpr uint32_t kPlanNoBlk = 128u;        // keep the [step][lane] code layout (no band walks)
 
 // Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
@@ -41,8 +42,12 @@ struct Plan {
     bool fused = false;  // int32-only plans: the fill kernel walks its own pair
     bool end_aligned = true;  // pass tasks ticketed end-aligned (not kPlanPassMajor)
     // local walks: 16 = lane walks (ta_walk_lane.h), 32 = two pairs per wave
-    // (ta_walk2.h), 0 = one pair per wave (traceback_pair)
+    // (ta_walk2.h), 64 = band walks (ta_walk_band.h, blk), 0 = one pair per wave
+    // (traceback_pair)
     int walk_group = 16;
+    // codes in the blocked layout (ta_layout.h blk_index): local plans of short
+    // pairs in equal-shape couples only (the band walk's layout)
+    bool blk = false;
     std::vector<uint32_t> qlen, tlen;
     std::vector<uint32_t> order;    // traceback order (all pairs)
     std::vector<uint32_t> singles;  // int32 fill: pair ids

@@ -1,0 +1,442 @@
+// bioinfo1_amd/csrc/ta_walk_band.h -- the local-mode traceback of plans in the
+// blocked code layout (ta_layout.h blk_index): ONE LANE PER PAIR, 64 walks per
+// one-wave block, every operand of a walk step in the lane's own LDS region,
+// then one wave per pair formats the runs into the CIGAR slot.
+//
+// Same walk as traceback_pair<kLocal> (ta_device.h) and the lane walk
+// (ta_walk_lane.h): from the goal, while the current cell's cost is > 0
+// (team_alignment.cpp:201-217), move to the parent its code names (D wins over
+// I: the packed fill stores raw compares), the cost tracked exactly (a cell
+// with cost > 0 is unclamped, so its parent's cost is its own minus the step's
+// score, :20-28).  For gap <= 0 and sequences without '-' (the planner and the
+// dual fill's per-pair flag route everything else to the fallback walk), a
+// gap move never lowers the cost, so the walk can only end right after a
+// diagonal move.
+//
+// One iteration resolves the D run above the current cell inside its stripe
+// from ONE code dword (the D plane shifted so that the current row is bit 0:
+// trailing ones), then the M or I move at the row the run stops on.  A walk
+// follows its stripe (16 rows) along the steps, which in the blocked layout are
+// contiguous: a stripe's 64-step window is 4 x 64 bytes.  Each walker stages
+// the windows of the stripes ahead of it -- predicted along the diagonal from
+// its current cell -- into a ring of 4 slots (stripe & 3).  A slot is
+// addressed by position alone (codes at step & 63, target bytes at their
+// address & 127), and carries its stripe and window start in a header read
+// beside the data, so a step needs no per-slot bookkeeping in registers.
+// Staging runs in rounds: every kBwRound iterations all lanes write the
+// registers they loaded in the previous round into their slot (the loads had a
+// whole round to land) and issue the loads of the next stripe, so no walker
+// waits on memory unless its path left its predicted window (it then sits out
+// until its stripe is restaged around its actual cell).  Runs go to an LDS list
+// per walker, leave for HBM 16 at a time, and format_runs_kernel turns them
+// into the CIGAR text (the RunWriter layout, ta_device.h).
+#pragma once
+
+#include "ta_walk_lane.h"
+
+namespace ta {
+namespace {
+
+#ifdef TA_BW_PROF
+// experiment builds only: per-phase clock totals of the band walk
+__device__ unsigned long long bw_prof[8];
+#define BW_T(v) const uint64_t v = __builtin_readcyclecounter()
+#define BW_ACC(k, d) bwp[k] += (d)
+#else
+#define BW_T(v)
+#define BW_ACC(k, d)
+#endif
+
+constexpr int kBwSlots = 4;                       // stripe slots per walker (ring: stripe & 3)
+constexpr int kBwWin = 64;                        // code window: 64 steps = 4 blocks of 16
+constexpr int kBwT = kBwWin * 4;                  // slot offset: target ring (128 bytes, by address & 127)
+constexpr int kBwQ = kBwT + 128;                  // slot offset: the stripe's 16 query bytes
+constexpr int kBwHdr = kBwQ + 16;                 // slot offset: header {stripe, window start step}
+constexpr int kBwSlotB = 512;                     // bytes per slot
+constexpr int kBwRunCap = 64;                     // event list: two halves of 32, leaving for HBM by halves
+#ifndef TA_BW_COLS
+#define TA_BW_COLS 2
+#endif
+constexpr int kBwCols = TA_BW_COLS;               // columns a walk iteration may move (1 or 2)
+constexpr int kBwRound = 8 / kBwCols;             // walk iterations per staging round (<= 16 events)
+constexpr int kBwLook = 3;                        // stripes staged ahead of the walk
+constexpr int kBwRuns = kBwSlots * kBwSlotB;      // region offset of the run list
+constexpr int kBwRegion = kBwRuns + kBwRunCap * 4 + 16;  // 2320 = 580 dwords (4 mod 32: spreads banks)
+static_assert(kBwRegion % 16 == 0 && kBwHdr + 8 <= kBwSlotB, "band walk LDS layout");
+
+// Registers of one stripe staged in flight: 16 code pieces (4 blocks x 64
+// bytes), 32 query bytes and 80 target bytes from 16-byte aligned addresses.
+struct BwStage {
+    uint4 c[16];
+    uint4 q[2];
+    uint4 t[5];
+};
+
+typedef unsigned int bw_v4 __attribute__((ext_vector_type(4)));
+typedef unsigned int bw_v2 __attribute__((ext_vector_type(2)));
+typedef __attribute__((address_space(3))) bw_v4 lds_u128;
+typedef __attribute__((address_space(3))) bw_v2 lds_u64;
+typedef __attribute__((address_space(3))) uint8_t lds_u8t;
+__device__ __forceinline__ uint4 lds_ld128(uint32_t a) {
+    const bw_v4 v = *(const lds_u128*)(uintptr_t)a;
+    return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ void lds_st128(uint32_t a, uint4 v) {
+    bw_v4 w;
+    w.x = v.x, w.y = v.y, w.z = v.z, w.w = v.w;
+    *(lds_u128*)(uintptr_t)a = w;
+}
+__device__ __forceinline__ bw_v2 lds_ld64(uint32_t a) { return *(const lds_u64*)(uintptr_t)a; }
+__device__ __forceinline__ void lds_st64(uint32_t a, int x, int y) {
+    bw_v2 w;
+    w.x = (uint32_t)x, w.y = (uint32_t)y;
+    *(lds_u64*)(uintptr_t)a = w;
+}
+__device__ __forceinline__ uint32_t lds_ld8(uint32_t a) { return *(const lds_u8t*)(uintptr_t)a; }
+
+// 16-byte pieces from [lo, hi] (16-byte aligned bounds that hold valid bytes):
+// a piece outside holds a clamped copy -- never read by the walk, and never a
+// fault (it lies on the same page as a valid byte).
+__device__ __forceinline__ uint4 bw_piece(uintptr_t a, uintptr_t lo, uintptr_t hi) {
+    a = a < lo ? lo : (a > hi ? hi : a);
+    return *reinterpret_cast<const uint4*>(a);
+}
+
+// Window of stripe h (global stripe index: pass * 64 + lane) centred on column
+// ctr: 4 blocks from u0 = floor((ctr + ln - 24) / 16), clamped to the pass.
+// Returns the window's first step; `ta16` the 16-byte aligned address of its
+// target pieces.
+__device__ __forceinline__ int bw_issue(BwStage& st, const uint32_t* P, const uint8_t* Q, const uint8_t* T,
+                                        uint32_t n, uint32_t m, uint32_t nb, int h, int ctr, uint32_t& qmis,
+                                        uint32_t& ta16) {
+    const uint32_t pass = (uint32_t)h >> 6, ln = (uint32_t)h & 63u;
+    int u0 = (ctr + (int)ln - 24) >> 4;
+    u0 = min(max(u0, 0), (int)nb - 4);  // nb >= 4: pass_steps(m) >= 64
+    const uint32_t* cp = P + blk_index(pass, 16u * (uint32_t)u0, ln, nb);
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            st.c[4 * b + k] = *reinterpret_cast<const uint4*>(cp + (uint64_t)b * (kWave * kBlkSteps) + 4 * k);
+    const uintptr_t qa = (uintptr_t)Q + 16u * (uint32_t)h, q16 = qa & ~(uintptr_t)15;
+    const uintptr_t qlo = (uintptr_t)Q & ~(uintptr_t)15, qhi = ((uintptr_t)Q + n - 1) & ~(uintptr_t)15;
+    qmis = (uint32_t)(qa - q16);
+    st.q[0] = bw_piece(q16, qlo, qhi);
+    st.q[1] = bw_piece(q16 + 16, qlo, qhi);
+    const int cw = 16 * u0 - (int)ln;  // the window's first column
+    const uintptr_t t16 = (uintptr_t)((intptr_t)T + cw) & ~(uintptr_t)15;
+    const uintptr_t tlo = (uintptr_t)T & ~(uintptr_t)15, thi = ((uintptr_t)T + m - 1) & ~(uintptr_t)15;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) st.t[k] = bw_piece(t16 + 16u * k, tlo, thi);
+    ta16 = (uint32_t)t16;
+    return 16 * u0;
+}
+
+// The staged stripe into its slot: codes at step & 63, target bytes at their
+// address & 127, the 16 query bytes shifted to the slot's query field, and the
+// header (stripe, first step) that tells a step whether its cell is inside.
+__device__ __forceinline__ void bw_commit(const BwStage& st, uint32_t sb, uint32_t qmis, uint32_t ta16, int h,
+                                          int w0) {
+#pragma unroll
+    for (int k = 0; k < 16; ++k) lds_st128(sb + ((uint32_t)(w0 * 4 + 16 * k) & 255u), st.c[k]);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) lds_st128(sb + kBwT + ((ta16 + 16u * k) & 127u), st.t[k]);
+    const uint32_t w[8] = {st.q[0].x, st.q[0].y, st.q[0].z, st.q[0].w, st.q[1].x, st.q[1].y, st.q[1].z, st.q[1].w};
+    const uint32_t a = qmis >> 2, sh = qmis & 3u;
+    uint32_t s[5];
+#pragma unroll
+    for (int i = 0; i < 5; ++i) {
+        const uint32_t v0 = w[i], v1 = w[i + 1], v2 = w[i + 2], v3 = i + 3 < 8 ? w[i + 3] : 0u;
+        s[i] = a == 0 ? v0 : (a == 1 ? v1 : (a == 2 ? v2 : v3));
+    }
+    uint4 o;
+    o.x = __builtin_amdgcn_alignbyte(s[1], s[0], sh);
+    o.y = __builtin_amdgcn_alignbyte(s[2], s[1], sh);
+    o.z = __builtin_amdgcn_alignbyte(s[3], s[2], sh);
+    o.w = __builtin_amdgcn_alignbyte(s[4], s[3], sh);
+    lds_st128(sb + kBwQ, o);
+    lds_st64(sb + kBwHdr, h, w0);
+}
+
+// One half (32 events) of the walker's list to its event words in HBM.
+__device__ __forceinline__ void bw_runs_out(uint32_t src, uint32_t* dst) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(dst + 4 * k) = lds_ld128(src + 16u * k);
+}
+
+// The local walks of pairs 64 * blockIdx.x + lane (one wave per block).
+// Events (op 0/1/2 = M/I/D in bits 1:0, count above; consecutive events of
+// one op are one CIGAR run, merged by format_runs) to a.runs; their number to
+// cigar_len (format_runs_kernel replaces it by the text length).
+__device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t* lds, int lane) {
+    const uint32_t k = 64u * blockIdx.x + (uint32_t)lane;
+    bool has = k < a.count;
+    const uint32_t p = has ? (a.order ? a.order[a.begin + k] : a.begin + k) : 0u;
+    if (has && a.pflag && a.pflag[p]) has = false;  // '-' bytes: the fallback walk (traceback_kernel)
+    uint32_t n = 0, m = 0, gi = 0, gj = 0;
+    int H = 0;
+    const uint32_t* P = a.ptrs;
+    const uint8_t* Q = a.qbytes;
+    const uint8_t* T = a.tbytes;
+    uint32_t* rout = a.runs;
+    if (has) {
+        n = a.qlen[p];
+        m = a.tlen[p];
+        gi = a.goal_i[p];
+        gj = a.goal_j[p];
+        H = a.score[p];
+        P += a.ptr_off[p];
+        Q += a.qoff[p];
+        T += a.toff[p];
+        rout += a.slot_off[p] >> 1;  // 4 (n + m) bytes <= 2 x the slot
+    }
+    const uint32_t nb = blk_count(m);
+    const int ma = a.match, mi = a.mismatch, gap = a.gap;
+    const uint32_t reg = lds_addr(lds) + (uint32_t)lane * kBwRegion;
+    const uint32_t rl = reg + kBwRuns;  // event list: 64 entries, two halves of 32
+    const uint32_t tlow = (uint32_t)(uintptr_t)T;  // target byte c lives at ring (tlow + c) & 127
+    bool live = has && H > 0;           // a positive score has its goal at i, j >= 1
+    int g = live ? (int)((gi - 1u) >> 4) : 0, r = live ? (int)((gi - 1u) & 15u) : 0, c = live ? (int)gj - 1 : 0;
+    // every slot's header invalid (stripe -1)
+#pragma unroll
+    for (int s = 0; s < kBwSlots; ++s) lds_st64(reg + s * kBwSlotB + kBwHdr, -1, 0);
+    BwStage st;
+    uint32_t qmis = 0, ta16 = 0;
+    // the goal's stripe, staged at once
+    if (live) {
+        const int w0 = bw_issue(st, P, Q, T, n, m, nb, g, c - r + 8, qmis, ta16);
+        bw_commit(st, reg + ((uint32_t)g & 3u) * kBwSlotB, qmis, ta16, g, w0);
+    }
+    int lo = g;                 // lowest stripe staged or in flight
+    bool pend = false, stalled = false;
+    int pend_h = 0, pend_w0 = 0;
+    uint32_t nr = 0u, nout = 0u;  // events listed, events in HBM
+#ifdef TA_BW_PROF
+    uint64_t bwp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+    BW_T(t_begin);
+    while (ballot(live)) {
+        // ---- staging round: commit what the last round loaded, issue the next stripe
+        BW_T(t0);
+        if (pend) {
+            bw_commit(st, reg + ((uint32_t)pend_h & 3u) * kBwSlotB, qmis, ta16, pend_h, pend_w0);
+            pend = false;
+            if (pend_h == g) stalled = false;
+        }
+        BW_T(t1);
+        BW_ACC(0, t1 - t0);
+        int h = -1, ctr = 0;
+        if (live) {
+            if (stalled) {  // the walk left its window: restage its stripe around the current cell
+                h = g;
+                ctr = c - r + 8;
+            } else if (lo > g - kBwLook && lo > 0) {  // the next stripe ahead, on the diagonal
+                h = lo - 1;
+                ctr = c - r + 8 - 16 * (g - h);
+            }
+        }
+        if (h >= 0) {
+            pend_w0 = bw_issue(st, P, Q, T, n, m, nb, h, ctr, qmis, ta16);
+            pend_h = h;
+            pend = true;
+            lo = min(lo, h);
+        }
+        // a full half of the event list to HBM (at most 16 events per round)
+        if (nr - nout >= 32u) {
+            bw_runs_out(rl + ((nout & 32u) << 2), rout + nout);
+            nout += 32u;
+        }
+        BW_T(t2);
+        BW_ACC(1, t2 - t1);
+        BW_ACC(5, 1);
+        // ---- walk iterations: the LDS reads of a step go out together (pinned
+        // ahead of the one divergent block), a walk that leaves its staged window
+        // stops there until its stripe is restaged.  With kBwCols = 2 a step also
+        // reads the next column's code and target byte and, when the first move
+        // stays in the stripe, makes the second move too.
+#pragma unroll
+        for (int it = 0; it < kBwRound; ++it) {
+#ifdef TA_BW_PROF
+            bwp[6] += (live && stalled) ? 1 : 0;
+            bwp[7] += (live && !stalled) ? 1 : 0;
+#endif
+            const uint32_t ln = (uint32_t)g & 63u, t = (uint32_t)c + ln;
+            const uint32_t sb = reg + (((uint32_t)g & 3u) << 9);
+            bw_v2 hd = lds_ld64(sb + kBwHdr);
+            uint32_t x = lds_ld32(sb + ((t & 63u) << 2));
+            uint4 q4 = lds_ld128(sb + kBwQ);
+            uint32_t tb = lds_ld8(sb + kBwT + ((tlow + (uint32_t)c) & 127u));
+            uint32_t x1 = 0, tb1 = 0;
+            if constexpr (kBwCols == 2) {
+                x1 = lds_ld32(sb + (((t - 1u) & 63u) << 2));
+                tb1 = lds_ld8(sb + kBwT + ((tlow + (uint32_t)c - 1u) & 127u));
+            }
+            // (keeps the reads together: hipcc would otherwise sink the query and
+            // target reads behind the D-run test, a second round trip)
+            asm volatile("" : "+v"(hd), "+v"(x), "+v"(q4.x), "+v"(q4.y), "+v"(q4.z), "+v"(q4.w), "+v"(tb), "+v"(x1),
+                         "+v"(tb1));
+            stalled = stalled || (live && ((int)hd.x != g || t - hd.y >= (uint32_t)kBwWin));
+            if (live && !stalled) {
+                // one column: the D run from row rr up (bit planes, ta_internal.h Code:
+                // row rr's D at 31 - rr), then the M or I move at the row it stops on
+                auto column = [&](uint32_t xc, uint32_t tbc, int rr, int& Hc, uint32_t& nrc, int& nrow, bool& topc) {
+                    const uint32_t dp = xc >> (31 - rr);
+                    const int kd = (int)__builtin_ctz(~dp);  // <= rr + 1
+                    const bool top = kd > rr;                // the run leaves the stripe at its top
+                    const int rp = rr - kd;
+                    const uint32_t ib = (xc >> ((uint32_t)(15 - rp) & 31u)) & 1u;
+                    const uint32_t sel = (uint32_t)rp & 7u;
+                    const uint32_t qlo = __builtin_amdgcn_perm(q4.y, q4.x, sel), qhi = __builtin_amdgcn_perm(q4.w, q4.z, sel);
+                    const uint32_t qb = ((rp & 8) ? qhi : qlo) & 0xFFu;
+                    const int sc = (qb == tbc) ? ma : mi;
+                    const int mv = top ? 0 : (ib ? gap : sc);
+                    Hc -= __mul24(kd, gap) + mv;
+                    // events: the D run (if any), then the move (unless the run left the stripe)
+                    const uint32_t evm = ib | 4u;  // I or M, count 1
+                    const uint32_t ev0 = kd > 0 ? (2u | ((uint32_t)kd << 2)) : evm;
+                    lds_st32(rl + ((nrc & 63u) << 2), ev0);  // (past the end when not counted)
+                    lds_st32(rl + (((nrc + 1u) & 63u) << 2), evm);
+                    nrc += (uint32_t)(kd > 0) + (uint32_t)!top;
+                    nrow = rp - ((!top && !ib) ? 1 : 0);
+                    topc = top;
+                };
+                int nrow;
+                bool top;
+                column(x, tb, r, H, nr, nrow, top);
+                if constexpr (kBwCols == 2) {
+                    // the second column: the move stayed in the stripe, the walk goes on,
+                    // and column c - 1 is inside the window
+                    const bool two = !top && nrow >= 0 && H > 0 && t - 1u - hd.y < (uint32_t)kBwWin;
+                    int H2 = H, nrow2;
+                    uint32_t nr2 = nr;
+                    bool top2;
+                    column(x1, tb1, nrow, H2, nr2, nrow2, top2);
+                    c -= top ? 0 : 1;
+                    c -= (two && !top2) ? 1 : 0;
+                    nrow = two ? nrow2 : nrow;
+                    H = two ? H2 : H;
+                    nr = two ? nr2 : nr;
+                } else {
+                    c -= top ? 0 : 1;
+                }
+                // the next cell: up the stripe (D run), left (I) or diagonal (M)
+                g += nrow >> 31;  // -1 when the row leaves the stripe's top
+                r = nrow & 15;    // (-1 -> 15)
+                live = H > 0;
+            }
+        }
+        BW_T(t3);
+        BW_ACC(3, t3 - t2);
+    }
+    BW_T(t_end);
+    BW_ACC(4, t_end - t_begin);
+#ifdef TA_BW_PROF
+    // phases: per wave (lane 0); stall / walk iterations: summed over lanes
+    if (lane == 0)
+        for (int q = 0; q < 6; ++q) atomicAdd(&bw_prof[q], (unsigned long long)bwp[q]);
+    atomicAdd(&bw_prof[6], (unsigned long long)bwp[6]);
+    atomicAdd(&bw_prof[7], (unsigned long long)bwp[7]);
+#endif
+    if (has) {
+        // the rest of the list (fewer than 48 events, in list order)
+        for (uint32_t j = nout; j < nr; ++j) rout[j] = lds_ld32(rl + ((j & 63u) << 2));
+        a.cigar_len[p] = nr;  // the event count, for format_runs_kernel
+    }
+}
+
+// Decimal digits of c (c < 2^32).
+__device__ __forceinline__ uint32_t bw_digits(uint32_t c) {
+    uint32_t d = 1u + (c >= 10u) + (c >= 100u) + (c >= 1000u) + (c >= 10000u);
+    if (ballot(c >= 100000u))
+        d += (c >= 100000u) + (c >= 1000000u) + (c >= 10000000u) + (c >= 100000000u) + (c >= 1000000000u);
+    return d;
+}
+
+// "<count><op>" at q (digits first).
+__device__ __forceinline__ void bw_put_run(char* q, uint32_t c, uint32_t op, uint32_t digits, bool act) {
+    if (act) q[digits] = (char)((0x44494Du >> (8u * op)) & 0xFFu);  // 'M', 'I', 'D'
+    for (uint32_t d = 0; ballot(act && d < digits); ++d) {
+        if (act && d < digits) {
+            const uint32_t qv = __umulhi(c, 0xCCCCCCCDu) >> 3;  // c / 10
+            q[digits - 1u - d] = (char)('0' + (c - 10u * qv));
+            c = qv;
+        }
+    }
+}
+
+// One wave per pair of a band-walked chunk: its events (in walk order, i.e.
+// the CIGAR's last run first; consecutive events of one op are one run)
+// merged into runs and formatted right to left into the end of its slot, 64
+// events per round (RunWriter's layout, ta_device.h; "1\0" for no move,
+// :145-160).  A run still open at the end of a round is carried into the next.
+__device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int lane) {
+    if (a.pflag && a.pflag[p]) return;  // walked by the fallback walk
+    const uint32_t n = a.qlen[p], m = a.tlen[p];
+    const uint64_t cap = cigar_slot_bytes(n, m), soff = a.slot_off[p];
+    const uint32_t* ev = a.runs + (soff >> 1);
+    char* end = a.slots + soff + cap;
+    const uint32_t E = a.cigar_len[p];
+    uint32_t used = 0;
+    if (E == 0) {
+        if (lane == 0) {
+            *(end - 2) = '1';
+            *(end - 1) = '\0';
+        }
+        used = 2;
+    }
+    uint32_t cop = 3u, ccnt = 0u;  // the run carried from the previous round (op 3: none)
+    for (uint32_t base = 0; base < E; base += 64u) {
+        const uint32_t k = base + (uint32_t)lane;
+        const bool act = k < E;
+        const uint32_t v = act ? ev[k] : 3u;  // (op 3 past the end: a run boundary)
+        const uint32_t op = v & 3u;
+        const uint32_t op0 = (uint32_t)__shfl((int)op, 0, 64);
+        if (cop != 3u && op0 != cop) {  // the carried run ended with the last round: its text first
+            const uint32_t dg = bw_digits(ccnt);
+            bw_put_run(end - used - (dg + 1u), ccnt, cop, dg, lane == 0);
+            used += dg + 1u;
+            cop = 3u;
+            ccnt = 0u;
+        }
+        // run sums: an inclusive prefix sum of the counts, minus the prefix
+        // before each lane's run head (the carried count joins lane 0's run)
+        const uint32_t prev = lane == 0 ? cop : (uint32_t)__shfl_up((int)op, 1, 64);
+        const uint64_t heads = ballot(op != prev);
+        const uint32_t cntv = (v >> 2) + (lane == 0 ? ccnt : 0u);
+        uint32_t pre = cntv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
+            if (lane >= o) pre += y;
+        }
+        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
+        const uint64_t hb = heads & upto;
+        const int hs = hb ? 63 - __clzll((long long)hb) : 0;  // this lane's run head (lane 0 continues the carry)
+        const uint32_t before = (uint32_t)__shfl((int)pre, hs > 0 ? hs - 1 : 0, 64);
+        const uint32_t sum = pre - (hs > 0 ? before : 0u);
+        // a run ends at lane k when the next event has another op; lane 63's run
+        // continues into the next round unless it is the last event
+        const uint32_t nop = (uint32_t)__shfl_down((int)op, 1, 64);
+        const bool ends = act && (lane == 63 ? k + 1 == E : nop != op);
+        const uint32_t dg = bw_digits(sum);
+        const uint32_t L = ends ? dg + 1u : 0u;
+        uint32_t incl = L;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        bw_put_run(end - used - incl, sum, op, dg, ends);
+        used += (uint32_t)__shfl((int)incl, 63, 64);
+        const bool cont = base + 64u < E;  // lane 63's run, carried
+        cop = cont ? (uint32_t)__shfl((int)op, 63, 64) : 3u;
+        ccnt = cont ? (uint32_t)__shfl((int)sum, 63, 64) : 0u;
+    }
+    if (lane == 0) {
+        a.cigar_start[p] = soff + cap - used;
+        a.cigar_len[p] = used;
+    }
+}
+
+}  // namespace
+}  // namespace ta

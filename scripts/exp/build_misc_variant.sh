@@ -9,7 +9,7 @@ NAME=$1; shift
 mkdir -p "$B/exp"
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-unused-function "$@" \
   -DTA_TU_MISC -c "$CS/ta_kernels.hip" -o "$B/exp/misc_$NAME.o"
-/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o \
+/opt/rocm/bin/hipcc -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_dual_blk.o" \
   "$B"/ta_flex_{0,1,2}{0,1}.o "$B/exp/misc_$NAME.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_server.o" "$B/ta_planner.o" "$B/shim.o" \
   -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$B/exp/$NAME.so"
 echo "built $B/exp/$NAME.so"

@@ -9,7 +9,7 @@ import pytest
 from conftest import DIGESTS, ROOT, STRIDED, cigar_digest, digest_batch, load_digest, run_plan
 
 from bioinfo1_amd import synth
-from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_SERIAL_PASSES, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2, Aligner, DevicePlan,
+from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_BLK, TA_PLAN_NO_FLEX, TA_PLAN_SERIAL_PASSES, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2, Aligner, DevicePlan,
                                 align)
 from oracle.pyoracle import Oracle
 
@@ -453,6 +453,45 @@ def test_local_group_walk_dual_and_fallback(aligner, oracle, sc):
         np.testing.assert_array_equal(got.target_begins, want.target_begins)
         for p in range(b.n_pairs):
             assert got.cigar(p) == want.cigar(p), (sc, flags, p)
+
+
+# Band walks (ta_walk_band.h) over the blocked code layout: local plans of
+# equal-shape couples only.  (scoring, query alphabet, target alphabet, shapes
+# -- each taken an even number of times, so every pair couples --, walk kind)
+BAND_CASES = [
+    ((1, -1, -1), b"ACGT", b"ACGT", [(1000, 1000)] * 16, 64),           # config 2's shape
+    ((1, -1, -1), b"ACGT", b"ACGT", [(1, 1), (5, 9), (16, 16), (17, 3), (64, 300), (15, 1), (1, 200), (300, 1)], 64),
+    ((2, -3, -1), b"ACGTN", b"acgtN", [(1030, 900), (2100, 700), (1500, 600)], 64),  # across passes; N, lowercase
+    ((3, 4, 0), b"ACGT", b"ACGT", [(300, 280), (64, 64)], 64),          # mismatch above match, free gaps
+    ((5, -4, -3), b"AC", b"ACGT", [(257, 255), (1024, 1024)], 64),
+    ((1, -1, -1), b"AC-GT", b"ACGT-", [(200, 180), (700, 650)], 64),     # '-': handed back, the fallback walk
+    ((2, -1, 2), b"ACGT", b"ACGT", [(300, 280), (64, 64)], 0),           # gap > 0: one-pair walk, blocked layout
+]
+
+
+@pytest.mark.parametrize("case", range(len(BAND_CASES)))
+def test_band_walk(aligner, oracle, case):
+    sc, qa, ta, shapes, walk = BAND_CASES[case]
+    rng = np.random.default_rng(0xBA4D + case)
+    qa, ta = np.frombuffer(qa, np.uint8), np.frombuffer(ta, np.uint8)
+    pairs = []
+    for k in range(2 * len(shapes) * 4):
+        n, m = shapes[(k // 2) % len(shapes)]
+        pairs.append((qa[rng.integers(len(qa), size=n)].tobytes(), ta[rng.integers(len(ta), size=m)].tobytes()))
+    if case == 0:  # plus related pairs: long match runs, long walks
+        rb = synth.related_batch(32, 1000, 1000, seed=0xBA4E)
+        pairs += [(rb.query(p), rb.target(p)) for p in range(rb.n_pairs)]
+    b = synth.from_pairs(pairs)
+    plan = DevicePlan(aligner, b, 1, *sc, True)
+    assert plan.blk and plan.walk == walk, (plan.blk, plan.walk)
+    plan.close()
+    want = oracle.align_batch(b, 1, *sc, True)
+    for flags in (0, TA_PLAN_NO_BLK):
+        got = run_plan(aligner, b, 1, sc, True, flags)
+        np.testing.assert_array_equal(got.scores, want.scores)
+        np.testing.assert_array_equal(got.target_begins, want.target_begins)
+        for p in range(b.n_pairs):
+            assert got.cigar(p) == want.cigar(p), (case, flags, p, b.qlen[p], b.tlen[p])
 
 
 def test_local_walk_long_runs(aligner, oracle):
