@@ -315,8 +315,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             if constexpr (BLK) {
                 const uint32_t sl = (t & 15u) * kWave + (uint32_t)lane;
                 io.cbuf[sl] = cA;
-                io.cbuf[kBlkSteps * kWave + sl] = cB;
-                if ((t & 15u) == 15u || t + 1 == steps) blk_flush(t >> 4);
+                io.cbuf[kBlkSteps * kWave + sl] = cB;  // (flushed by run_steps)
             } else {
                 // 32-bit byte offset from the uniform row base (SGPR base + VGPR offset stores)
                 const uint32_t off = (t * kWave + (uint32_t)lane) * 4u;
@@ -335,12 +334,17 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 reload(t);
                 next_reload += 64;
             }
-            const uint32_t blk = min(t_end, next_reload);
+            uint32_t blk = min(t_end, next_reload);
+            // BLK: stop at each 16-step block end, flushing outside the step body
+            // (a branch inside it costs the whole step loop spills)
+            if constexpr (BLK) blk = min(blk, (t | 15u) + 1u);
             for (; t + 1 < blk; t += 2) {
                 step(t, masked_tag);
                 step(t + 1, masked_tag);
             }
             if (t < blk) step(t++, masked_tag);
+            if constexpr (BLK)
+                if ((t & 15u) == 0 || t == steps) blk_flush((t - 1) >> 4);
         }
     };
     run_steps(ramp_end, std::true_type{});

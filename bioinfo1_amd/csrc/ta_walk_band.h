@@ -58,7 +58,7 @@ constexpr int kBwRunCap = 64;                     // event list: two halves of 3
 #define TA_BW_COLS 2
 #endif
 constexpr int kBwCols = TA_BW_COLS;               // columns a walk iteration may move (1 or 2)
-constexpr int kBwRound = 8 / kBwCols;             // walk iterations per staging round (<= 16 events)
+constexpr int kBwRound = 8 / kBwCols;             // walk iterations per staging round (<= 8 events)
 constexpr int kBwLook = 3;                        // stripes staged ahead of the walk
 constexpr int kBwRuns = kBwSlots * kBwSlotB;      // region offset of the run list
 constexpr int kBwRegion = kBwRuns + kBwRunCap * 4 + 16;  // 2320 = 580 dwords (4 mod 32: spreads banks)
@@ -94,18 +94,13 @@ __device__ __forceinline__ void lds_st64(uint32_t a, int x, int y) {
 }
 __device__ __forceinline__ uint32_t lds_ld8(uint32_t a) { return *(const lds_u8t*)(uintptr_t)a; }
 
-// 16-byte pieces from [lo, hi] (16-byte aligned bounds that hold valid bytes):
-// a piece outside holds a clamped copy -- never read by the walk, and never a
-// fault (it lies on the same page as a valid byte).
-__device__ __forceinline__ uint4 bw_piece(uintptr_t a, uintptr_t lo, uintptr_t hi) {
-    a = a < lo ? lo : (a > hi ? hi : a);
-    return *reinterpret_cast<const uint4*>(a);
-}
-
 // Window of stripe h (global stripe index: pass * 64 + lane) centred on column
 // ctr: 4 blocks from u0 = floor((ctr + ln - 24) / 16), clamped to the pass.
 // Returns the window's first step; `ta16` the 16-byte aligned address of its
-// target pieces.
+// target pieces.  The query and target pieces are 16-byte aligned and clamped
+// to [first, last] piece that holds a valid byte (32-bit offsets from the
+// pair's aligned base): a clamped piece is never read by the walk, and never
+// a fault.
 __device__ __forceinline__ int bw_issue(BwStage& st, const uint32_t* P, const uint8_t* Q, const uint8_t* T,
                                         uint32_t n, uint32_t m, uint32_t nb, int h, int ctr, uint32_t& qmis,
                                         uint32_t& ta16) {
@@ -118,17 +113,23 @@ __device__ __forceinline__ int bw_issue(BwStage& st, const uint32_t* P, const ui
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             st.c[4 * b + k] = *reinterpret_cast<const uint4*>(cp + (uint64_t)b * (kWave * kBlkSteps) + 4 * k);
-    const uintptr_t qa = (uintptr_t)Q + 16u * (uint32_t)h, q16 = qa & ~(uintptr_t)15;
-    const uintptr_t qlo = (uintptr_t)Q & ~(uintptr_t)15, qhi = ((uintptr_t)Q + n - 1) & ~(uintptr_t)15;
-    qmis = (uint32_t)(qa - q16);
-    st.q[0] = bw_piece(q16, qlo, qhi);
-    st.q[1] = bw_piece(q16 + 16, qlo, qhi);
+    // query: 32 bytes from the aligned piece holding row 16h
+    const uint8_t* qb = (const uint8_t*)((uintptr_t)Q & ~(uintptr_t)15);
+    const uint32_t qm = (uint32_t)(uintptr_t)Q & 15u;
+    const uint32_t qo = (qm + 16u * (uint32_t)h) & ~15u, qhi = (qm + n - 1u) & ~15u;
+    qmis = (qm + 16u * (uint32_t)h) & 15u;
+    st.q[0] = *reinterpret_cast<const uint4*>(qb + min(qo, qhi));
+    st.q[1] = *reinterpret_cast<const uint4*>(qb + min(qo + 16u, qhi));
+    // target: 80 bytes from the aligned piece holding the window's first column
+    const uint8_t* tb = (const uint8_t*)((uintptr_t)T & ~(uintptr_t)15);
+    const int tm = (int)((uint32_t)(uintptr_t)T & 15u);
     const int cw = 16 * u0 - (int)ln;  // the window's first column
-    const uintptr_t t16 = (uintptr_t)((intptr_t)T + cw) & ~(uintptr_t)15;
-    const uintptr_t tlo = (uintptr_t)T & ~(uintptr_t)15, thi = ((uintptr_t)T + m - 1) & ~(uintptr_t)15;
+    const int thi = (tm + (int)m - 1) & ~15;
+    const int to = (tm + cw) & ~15;  // (floor; pieces outside the pair hold clamped copies, never read)
 #pragma unroll
-    for (int k = 0; k < 5; ++k) st.t[k] = bw_piece(t16 + 16u * k, tlo, thi);
-    ta16 = (uint32_t)t16;
+    for (int k = 0; k < 5; ++k) st.t[k] = *reinterpret_cast<const uint4*>(tb + min(max(to + 16 * k, 0), thi));
+    // ring positions follow the unclamped pieces' addresses
+    ta16 = (uint32_t)(uintptr_t)tb + (uint32_t)to;
     return 16 * u0;
 }
 
@@ -164,10 +165,11 @@ __device__ __forceinline__ void bw_runs_out(uint32_t src, uint32_t* dst) {
     for (int k = 0; k < 8; ++k) *reinterpret_cast<uint4*>(dst + 4 * k) = lds_ld128(src + 16u * k);
 }
 
-// The local walks of pairs 64 * blockIdx.x + lane (one wave per block).
-// Events (op 0/1/2 = M/I/D in bits 1:0, count above; consecutive events of
-// one op are one CIGAR run, merged by format_runs) to a.runs; their number to
-// cigar_len (format_runs_kernel replaces it by the text length).
+// The local walks of pairs 64 * blockIdx.x + lane (one wave per block).  One
+// event per walked column to a.runs: the D run's length above bit 2, the move
+// after it in bits 1:0 (0 M, 1 I, 3 none: the run left the stripe); their
+// number to cigar_len (format_runs_kernel merges them into runs and replaces
+// it by the text length).
 __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t* lds, int lane) {
     const uint32_t k = 64u * blockIdx.x + (uint32_t)lane;
     bool has = k < a.count;
@@ -214,6 +216,9 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
 #ifdef TA_BW_PROF
     uint64_t bwp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
+    // the scores in VGPRs (a select reads at most one SGPR besides its mask)
+    int mav = ma, miv = mi, gapv = gap;
+    asm volatile("" : "+v"(mav), "+v"(miv), "+v"(gapv));
     BW_T(t_begin);
     while (ballot(live)) {
         // ---- staging round: commit what the last round loaded, issue the next stripe
@@ -241,7 +246,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
             pend = true;
             lo = min(lo, h);
         }
-        // a full half of the event list to HBM (at most 16 events per round)
+        // a full half of the event list to HBM (at most 8 events per round)
         if (nr - nout >= 32u) {
             bw_runs_out(rl + ((nout & 32u) << 2), rout + nout);
             nout += 32u;
@@ -249,11 +254,14 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
         BW_T(t2);
         BW_ACC(1, t2 - t1);
         BW_ACC(5, 1);
-        // ---- walk iterations: the LDS reads of a step go out together (pinned
-        // ahead of the one divergent block), a walk that leaves its staged window
-        // stops there until its stripe is restaged.  With kBwCols = 2 a step also
-        // reads the next column's code and target byte and, when the first move
-        // stays in the stripe, makes the second move too.
+        // ---- walk iterations, branch-free: every lane computes both columns and
+        // writes both events (an event past the count is overwritten later; the
+        // list never holds more than 39 pending), and only the lanes whose cell
+        // is inside their staged window keep the results.  The LDS reads of a
+        // step go out together; a walk that leaves its window stops there until
+        // its stripe is restaged.  With kBwCols = 2 a step also reads the next
+        // column's code and target byte and, when the first move stays in the
+        // stripe, makes the second move too.
 #pragma unroll
         for (int it = 0; it < kBwRound; ++it) {
 #ifdef TA_BW_PROF
@@ -262,68 +270,76 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
 #endif
             const uint32_t ln = (uint32_t)g & 63u, t = (uint32_t)c + ln;
             const uint32_t sb = reg + (((uint32_t)g & 3u) << 9);
+            const uint32_t tr = sb + kBwT;
             bw_v2 hd = lds_ld64(sb + kBwHdr);
             uint32_t x = lds_ld32(sb + ((t & 63u) << 2));
             uint4 q4 = lds_ld128(sb + kBwQ);
-            uint32_t tb = lds_ld8(sb + kBwT + ((tlow + (uint32_t)c) & 127u));
+            uint32_t tb = lds_ld8(tr + ((tlow + (uint32_t)c) & 127u));
             uint32_t x1 = 0, tb1 = 0;
             if constexpr (kBwCols == 2) {
                 x1 = lds_ld32(sb + (((t - 1u) & 63u) << 2));
-                tb1 = lds_ld8(sb + kBwT + ((tlow + (uint32_t)c - 1u) & 127u));
+                tb1 = lds_ld8(tr + ((tlow + (uint32_t)c - 1u) & 127u));
             }
-            // (keeps the reads together: hipcc would otherwise sink the query and
-            // target reads behind the D-run test, a second round trip)
+            // (keeps the reads together ahead of their uses)
             asm volatile("" : "+v"(hd), "+v"(x), "+v"(q4.x), "+v"(q4.y), "+v"(q4.z), "+v"(q4.w), "+v"(tb), "+v"(x1),
                          "+v"(tb1));
-            stalled = stalled || (live && ((int)hd.x != g || t - hd.y >= (uint32_t)kBwWin));
-            if (live && !stalled) {
-                // one column: the D run from row rr up (bit planes, ta_internal.h Code:
-                // row rr's D at 31 - rr), then the M or I move at the row it stops on
-                auto column = [&](uint32_t xc, uint32_t tbc, int rr, int& Hc, uint32_t& nrc, int& nrow, bool& topc) {
-                    const uint32_t dp = xc >> (31 - rr);
-                    const int kd = (int)__builtin_ctz(~dp);  // <= rr + 1
-                    const bool top = kd > rr;                // the run leaves the stripe at its top
-                    const int rp = rr - kd;
-                    const uint32_t ib = (xc >> ((uint32_t)(15 - rp) & 31u)) & 1u;
-                    const uint32_t sel = (uint32_t)rp & 7u;
-                    const uint32_t qlo = __builtin_amdgcn_perm(q4.y, q4.x, sel), qhi = __builtin_amdgcn_perm(q4.w, q4.z, sel);
-                    const uint32_t qb = ((rp & 8) ? qhi : qlo) & 0xFFu;
-                    const int sc = (qb == tbc) ? ma : mi;
-                    const int mv = top ? 0 : (ib ? gap : sc);
-                    Hc -= __mul24(kd, gap) + mv;
-                    // events: the D run (if any), then the move (unless the run left the stripe)
-                    const uint32_t evm = ib | 4u;  // I or M, count 1
-                    const uint32_t ev0 = kd > 0 ? (2u | ((uint32_t)kd << 2)) : evm;
-                    lds_st32(rl + ((nrc & 63u) << 2), ev0);  // (past the end when not counted)
-                    lds_st32(rl + (((nrc + 1u) & 63u) << 2), evm);
-                    nrc += (uint32_t)(kd > 0) + (uint32_t)!top;
-                    nrow = rp - ((!top && !ib) ? 1 : 0);
-                    topc = top;
-                };
-                int nrow;
-                bool top;
-                column(x, tb, r, H, nr, nrow, top);
-                if constexpr (kBwCols == 2) {
-                    // the second column: the move stayed in the stripe, the walk goes on,
-                    // and column c - 1 is inside the window
-                    const bool two = !top && nrow >= 0 && H > 0 && t - 1u - hd.y < (uint32_t)kBwWin;
-                    int H2 = H, nrow2;
-                    uint32_t nr2 = nr;
-                    bool top2;
-                    column(x1, tb1, nrow, H2, nr2, nrow2, top2);
-                    c -= top ? 0 : 1;
-                    c -= (two && !top2) ? 1 : 0;
-                    nrow = two ? nrow2 : nrow;
-                    H = two ? H2 : H;
-                    nr = two ? nr2 : nr;
-                } else {
-                    c -= top ? 0 : 1;
-                }
+            const bool inwin = (int)hd.x == g && t - hd.y < (uint32_t)kBwWin;
+            const bool ok = live && !stalled && inwin;
+            stalled = stalled || (live && !inwin);
+            // one column: the D run from row rr up (bit planes, ta_internal.h Code:
+            // row rr's D at 31 - rr), then the M or I move at the row it stops on
+            // (none when the run leaves the stripe at its top); its event is the D
+            // run's length above bit 2, the move in bits 1:0 (3: none)
+            auto column = [&](uint32_t xc, uint32_t tbc, int rr, int& dH, uint32_t& ev, int& nrow, bool& top) {
+                const uint32_t dp = xc >> (31 - rr);
+                const int kd = (int)__builtin_ctz(~dp);  // <= rr + 1
+                const int rp = rr - kd;
+                top = rp < 0;
+                const uint32_t ib = (xc >> ((uint32_t)(15 - rp) & 31u)) & 1u;
+                const uint32_t sel = (uint32_t)rp & 7u;
+                const uint32_t qlo = __builtin_amdgcn_perm(q4.y, q4.x, sel), qhi = __builtin_amdgcn_perm(q4.w, q4.z, sel);
+                uint32_t qb = ((rp & 8) ? qhi : qlo) & 0xFFu;
+                // (computed in every lane: hipcc would branch around the query
+                // read for the lanes whose run left the stripe)
+                asm volatile("" : "+v"(qb));
+                const int sc = (qb == tbc) ? mav : miv;
+                const int mv = top ? 0 : (ib ? gapv : sc);
+                dH = __mul24(kd, gapv) + mv;
+                ev = ((uint32_t)kd << 2) | (top ? 3u : ib);
+                nrow = (top || ib) ? rp : rp - 1;
+            };
+            int dH1, nrow1;
+            uint32_t ev1;
+            bool top1;
+            column(x, tb, r, dH1, ev1, nrow1, top1);
+            lds_st32(rl + ((nr & 63u) << 2), ev1);
+            const int H1 = H - dH1;
+            if constexpr (kBwCols == 2) {
+                // the second column: the move stayed in the stripe, the walk goes on,
+                // and column c - 1 is inside the window
+                int dH2, nrow2;
+                uint32_t ev2;
+                bool top2;
+                column(x1, tb1, nrow1 & 15, dH2, ev2, nrow2, top2);
+                lds_st32(rl + (((nr + 1u) & 63u) << 2), ev2);
+                const bool two = ok && !top1 && nrow1 >= 0 && H1 > 0 && t - 1u - hd.y < (uint32_t)kBwWin;
+                const int dc = (top1 ? 0 : 1) + ((two && !top2) ? 1 : 0);
+                const int nrowf = two ? nrow2 : nrow1;
+                const int Hf = two ? H1 - dH2 : H1;
+                c -= ok ? dc : 0;
+                H = ok ? Hf : H;
+                nr += (ok ? 1u : 0u) + (two ? 1u : 0u);
                 // the next cell: up the stripe (D run), left (I) or diagonal (M)
-                g += nrow >> 31;  // -1 when the row leaves the stripe's top
-                r = nrow & 15;    // (-1 -> 15)
-                live = H > 0;
+                g += ok ? (nrowf >> 31) : 0;  // -1 when the row leaves the stripe's top
+                r = ok ? (nrowf & 15) : r;    // (-1 -> 15)
+            } else {
+                c -= (ok && !top1) ? 1 : 0;
+                H = ok ? H1 : H;
+                nr += ok ? 1u : 0u;
+                g += ok ? (nrow1 >> 31) : 0;
+                r = ok ? (nrow1 & 15) : r;
             }
+            live = live && H > 0;
         }
         BW_T(t3);
         BW_ACC(3, t3 - t2);
@@ -338,7 +354,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
     atomicAdd(&bw_prof[7], (unsigned long long)bwp[7]);
 #endif
     if (has) {
-        // the rest of the list (fewer than 48 events, in list order)
+        // the rest of the list (fewer than 40 events, in list order)
         for (uint32_t j = nout; j < nr; ++j) rout[j] = lds_ld32(rl + ((j & 63u) << 2));
         a.cigar_len[p] = nr;  // the event count, for format_runs_kernel
     }
@@ -364,9 +380,10 @@ __device__ __forceinline__ void bw_put_run(char* q, uint32_t c, uint32_t op, uin
     }
 }
 
-// One wave per pair of a band-walked chunk: its events (in walk order, i.e.
-// the CIGAR's last run first; consecutive events of one op are one run)
-// merged into runs and formatted right to left into the end of its slot, 64
+// One wave per pair of a band-walked chunk: its events (walk order, i.e. the
+// CIGAR's last run first) expanded into items -- the event's D run (when
+// long 1+), then its move (when any) -- and items of one op next to each other
+// merged into runs, formatted right to left into the end of its slot, 64
 // events per round (RunWriter's layout, ta_device.h; "1\0" for no move,
 // :145-160).  A run still open at the end of a round is carried into the next.
 __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int lane) {
@@ -376,6 +393,15 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
     const uint32_t* ev = a.runs + (soff >> 1);
     char* end = a.slots + soff + cap;
     const uint32_t E = a.cigar_len[p];
+#ifdef TA_BW_DUMP
+    // experiment builds only: the raw events, one byte each, as the "CIGAR"
+    for (uint32_t k = (uint32_t)lane; k < E; k += 64u) a.slots[soff + k] = (char)ev[k];
+    if (lane == 0) {
+        a.cigar_start[p] = soff;
+        a.cigar_len[p] = E;
+    }
+    return;
+#endif
     uint32_t used = 0;
     if (E == 0) {
         if (lane == 0) {
@@ -388,49 +414,73 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
     for (uint32_t base = 0; base < E; base += 64u) {
         const uint32_t k = base + (uint32_t)lane;
         const bool act = k < E;
-        const uint32_t v = act ? ev[k] : 3u;  // (op 3 past the end: a run boundary)
-        const uint32_t op = v & 3u;
-        const uint32_t op0 = (uint32_t)__shfl((int)op, 0, 64);
-        if (cop != 3u && op0 != cop) {  // the carried run ended with the last round: its text first
-            const uint32_t dg = bw_digits(ccnt);
-            bw_put_run(end - used - (dg + 1u), ccnt, cop, dg, lane == 0);
-            used += dg + 1u;
-            cop = 3u;
-            ccnt = 0u;
-        }
-        // run sums: an inclusive prefix sum of the counts, minus the prefix
-        // before each lane's run head (the carried count joins lane 0's run)
-        const uint32_t prev = lane == 0 ? cop : (uint32_t)__shfl_up((int)op, 1, 64);
-        const uint64_t heads = ballot(op != prev);
-        const uint32_t cntv = (v >> 2) + (lane == 0 ? ccnt : 0u);
-        uint32_t pre = cntv;
+        const uint32_t v = act ? ev[k] : 0u;
+        const uint32_t kd = v >> 2, mop = act ? (v & 3u) : 3u;
+        const bool va = kd > 0, vb = mop != 3u;      // item A: D x kd; item B: the move (M / I) x 1
+        const uint32_t first = va ? 2u : mop;        // op of the event's first / last item (3: no item)
+        const uint32_t last = vb ? mop : (va ? 2u : 3u);
+        // the previous event's last op (lane 0: the carried run's).  The shuffle
+        // stays outside the select: inside `?:` it becomes a branch that masks
+        // lane 0 off, and a bpermute reads 0 from a masked-off lane.
+        const uint32_t lup = (uint32_t)__shfl_up((int)last, 1, 64);
+        const uint32_t plast = lane == 0 ? cop : lup;
+        const uint32_t nfirst = (uint32_t)__shfl_down((int)first, 1, 64);  // (lane 63: unknown)
+        const bool ha = va && plast != 2u;                   // A starts a run
+        const bool hb = vb && (va || plast != mop);          // B starts a run (always after an A)
+        // item prefix sums: lane k's items end at pre_k; the carried count precedes lane 0
+        const uint32_t tot = kd + (vb ? 1u : 0u);
+        uint32_t pre = tot + (lane == 0 ? ccnt : 0u);
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
             if (lane >= o) pre += y;
         }
-        const uint64_t upto = lane == 63 ? ~0ull : ((2ull << lane) - 1ull);
-        const uint64_t hb = heads & upto;
-        const int hs = hb ? 63 - __clzll((long long)hb) : 0;  // this lane's run head (lane 0 continues the carry)
-        const uint32_t before = (uint32_t)__shfl((int)pre, hs > 0 ? hs - 1 : 0, 64);
-        const uint32_t sum = pre - (hs > 0 ? before : 0u);
-        // a run ends at lane k when the next event has another op; lane 63's run
-        // continues into the next round unless it is the last event
-        const uint32_t nop = (uint32_t)__shfl_down((int)op, 1, 64);
-        const bool ends = act && (lane == 63 ? k + 1 == E : nop != op);
-        const uint32_t dg = bw_digits(sum);
-        const uint32_t L = ends ? dg + 1u : 0u;
-        uint32_t incl = L;
+        const uint32_t preA = pre - (vb ? 1u : 0u);  // through item A
+        // the prefix just before the latest run head at or before each lane's end
+        // (a max scan: prefixes grow); the carried run's head sits at prefix 0
+        int hv = hb ? (int)(pre - 1u) : (ha ? (int)(preA - kd) : -1);
+        int hmax = hv;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const int y = __shfl_up(hmax, o, 64);
+            if (lane >= o) hmax = max(hmax, y);
+        }
+        const int hprev0 = __shfl_up(hmax, 1, 64);
+        const int hprev = lane == 0 ? 0 : max(hprev0, 0);  // (lane 0 continues the carry: head at 0)
+        const uint32_t sumA = preA - (uint32_t)(ha ? (int)(preA - kd) : hprev);
+        const uint32_t sumB = pre - (uint32_t)(hb ? (int)(pre - 1u) : hprev);
+        // run ends: A before B, or before the next event's first item of another op;
+        // lane 63's last item may continue into the next round
+        const bool more = lane == 63 && base + 64u < E;  // (lane 63 of a non-final round)
+        const bool nxt_diff = lane == 63 ? (base + 64u >= E) : nfirst != last;
+        const bool ea = act && va && (vb || (!more && nxt_diff));
+        const bool eb = act && vb && !more && nxt_diff;
+        const uint32_t dA = bw_digits(sumA), dB = bw_digits(sumB);
+        const uint32_t LA = ea ? dA + 1u : 0u, LB = eb ? dB + 1u : 0u;
+        uint32_t incl = LA + LB;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
             if (lane >= o) incl += y;
         }
-        bw_put_run(end - used - incl, sum, op, dg, ends);
+        // the carried run, when lane 0's first item does not continue it, ends first
+        const uint32_t f0 = (uint32_t)__shfl((int)first, 0, 64);
+        if (cop != 3u && f0 != cop) {
+            const uint32_t dg = bw_digits(ccnt);
+            bw_put_run(end - used - (dg + 1u), ccnt, cop, dg, lane == 0);
+            used += dg + 1u;
+        }
+        // lane k's texts: B (later in the walk) left of A
+        char* q = end - used - incl;
+        bw_put_run(q, sumB, mop, dB, eb);
+        bw_put_run(q + LB, sumA, 2u, dA, ea);
         used += (uint32_t)__shfl((int)incl, 63, 64);
-        const bool cont = base + 64u < E;  // lane 63's run, carried
-        cop = cont ? (uint32_t)__shfl((int)op, 63, 64) : 3u;
-        ccnt = cont ? (uint32_t)__shfl((int)sum, 63, 64) : 0u;
+        // carry lane 63's open run into the next round
+        const bool cont = base + 64u < E;
+        const uint32_t l63 = (uint32_t)__shfl((int)last, 63, 64);
+        const uint32_t s63 = (uint32_t)__shfl((int)(vb ? sumB : sumA), 63, 64);
+        cop = cont ? l63 : 3u;
+        ccnt = cont ? s63 : 0u;
     }
     if (lane == 0) {
         a.cigar_start[p] = soff + cap - used;

@@ -463,7 +463,7 @@ BAND_CASES = [
     ((1, -1, -1), b"ACGT", b"ACGT", [(1, 1), (5, 9), (16, 16), (17, 3), (64, 300), (15, 1), (1, 200), (300, 1)], 64),
     ((2, -3, -1), b"ACGTN", b"acgtN", [(1030, 900), (2100, 700), (1500, 600)], 64),  # across passes; N, lowercase
     ((3, 4, 0), b"ACGT", b"ACGT", [(300, 280), (64, 64)], 64),          # mismatch above match, free gaps
-    ((5, -4, -3), b"AC", b"ACGT", [(257, 255), (1024, 1024)], 64),
+    ((5, -4, -3), b"AC", b"ACGT", [(257, 255), (300, 280)], 64),        # (16 x 5 x min(n, m) within int16)
     ((1, -1, -1), b"AC-GT", b"ACGT-", [(200, 180), (700, 650)], 64),     # '-': handed back, the fallback walk
     ((2, -1, 2), b"ACGT", b"ACGT", [(300, 280), (64, 64)], 0),           # gap > 0: one-pair walk, blocked layout
 ]
