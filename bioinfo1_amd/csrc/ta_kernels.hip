@@ -925,8 +925,8 @@ __global__ __launch_bounds__(kWave) void traceback_lane_kernel(TraceArgs a) {
 
 // Local walks of blocked-layout plans, one lane per pair, 64 per one-wave
 // block (ta_walk_band.h).
-__global__ __launch_bounds__(kWave) void traceback_band_kernel(TraceArgs a) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kWave * kBwRegion];
+__global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void traceback_band_kernel(TraceArgs a) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[kWave * kBwRegion + kBwStageBytes];
     traceback_band_local(a, lds, (int)threadIdx.x);
 }
 

@@ -48,8 +48,12 @@ __device__ unsigned long long bw_prof[8];
 #endif
 
 constexpr int kBwSlots = 4;                       // stripe slots per walker (ring: stripe & 3)
-constexpr int kBwWin = 64;                        // code window: 64 steps = 4 blocks of 16
-constexpr int kBwT = kBwWin * 4;                  // slot offset: target ring (128 bytes, by address & 127)
+#ifndef TA_BW_BLOCKS
+#define TA_BW_BLOCKS 4
+#endif
+constexpr int kBwBlocks = TA_BW_BLOCKS;            // code window: 16-step blocks staged per stripe (3 or 4)
+constexpr int kBwWin = 16 * kBwBlocks;             // ... its steps (the ring holds 64)
+constexpr int kBwT = 64 * 4;                      // slot offset: target ring (128 bytes, by address & 127)
 constexpr int kBwQ = kBwT + 128;                  // slot offset: the stripe's 16 query bytes
 constexpr int kBwHdr = kBwQ + 16;                 // slot offset: header {stripe, window start step}
 constexpr int kBwSlotB = 512;                     // bytes per slot
@@ -57,20 +61,35 @@ constexpr int kBwRunCap = 64;                     // event list: two halves of 3
 #ifndef TA_BW_COLS
 #define TA_BW_COLS 2
 #endif
-constexpr int kBwCols = TA_BW_COLS;               // columns a walk iteration may move (1 or 2)
-constexpr int kBwRound = 8 / kBwCols;             // walk iterations per staging round (<= 8 events)
+constexpr int kBwCols = TA_BW_COLS;               // columns a walk iteration may move (1, 2 or 4)
+#ifndef TA_BW_EVENTS
+#define TA_BW_EVENTS 16
+#endif
+constexpr int kBwRound = TA_BW_EVENTS / kBwCols;  // walk iterations per staging round (<= 16 events)
 constexpr int kBwLook = 3;                        // stripes staged ahead of the walk
 constexpr int kBwRuns = kBwSlots * kBwSlotB;      // region offset of the run list
 constexpr int kBwRegion = kBwRuns + kBwRunCap * 4 + 16;  // 2320 = 580 dwords (4 mod 32: spreads banks)
 static_assert(kBwRegion % 16 == 0 && kBwHdr + 8 <= kBwSlotB, "band walk LDS layout");
+// pending events (< 32 after a round's flush, + one round's, + one spare write) within the list
+static_assert(31 + kBwRound * kBwCols + kBwCols - 1 < kBwRunCap, "band walk event list");
 
 // Registers of one stripe staged in flight: 16 code pieces (4 blocks x 64
 // bytes), 32 query bytes and 80 target bytes from 16-byte aligned addresses.
 struct BwStage {
-    uint4 c[16];
-    uint4 q[2];
-    uint4 t[5];
+    uint4 c[4 * kBwBlocks];
 };
+// The query and target pieces go global -> LDS directly (LDS-DMA, lane-linear:
+// piece k of lane l at stage + k * 1024 + 16 l), the codes through registers.
+// (Register destinations for all 23 pieces left hipcc copying some of them at
+// the branch merge, i.e. waiting for those loads in the middle of the issue.)
+constexpr int kBwTPieces = kBwBlocks + 1;  // target pieces: the window's columns from an aligned start
+constexpr int kBwStagePieces = 2 + kBwTPieces;  // + 2 query pieces
+constexpr int kBwStageBytes = kBwStagePieces * kWave * 16;
+typedef __attribute__((address_space(1))) const void* bw_gptr;
+typedef __attribute__((address_space(3))) void* bw_lptr;
+__device__ __forceinline__ void bw_dma16(const void* g, uint32_t lds) {
+    __builtin_amdgcn_global_load_lds((bw_gptr)g, (bw_lptr)(uintptr_t)lds, 16, 0, 0);
+}
 
 typedef unsigned int bw_v4 __attribute__((ext_vector_type(4)));
 typedef unsigned int bw_v2 __attribute__((ext_vector_type(2)));
@@ -101,48 +120,54 @@ __device__ __forceinline__ uint32_t lds_ld8(uint32_t a) { return *(const lds_u8t
 // to [first, last] piece that holds a valid byte (32-bit offsets from the
 // pair's aligned base): a clamped piece is never read by the walk, and never
 // a fault.
-__device__ __forceinline__ int bw_issue(BwStage& st, const uint32_t* P, const uint8_t* Q, const uint8_t* T,
-                                        uint32_t n, uint32_t m, uint32_t nb, int h, int ctr, uint32_t& qmis,
-                                        uint32_t& ta16) {
+__device__ __forceinline__ int bw_issue(BwStage& st, uint32_t stage, const uint32_t* P, const uint8_t* Q,
+                                        const uint8_t* T, uint32_t n, uint32_t m, uint32_t nb, int h, int ctr,
+                                        uint32_t& qmis, uint32_t& ta16) {
     const uint32_t pass = (uint32_t)h >> 6, ln = (uint32_t)h & 63u;
     int u0 = (ctr + (int)ln - 24) >> 4;
-    u0 = min(max(u0, 0), (int)nb - 4);  // nb >= 4: pass_steps(m) >= 64
+    u0 = min(max(u0, 0), (int)nb - kBwBlocks);  // nb >= 4: pass_steps(m) >= 64
     const uint32_t* cp = P + blk_index(pass, 16u * (uint32_t)u0, ln, nb);
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < kBwBlocks; ++b)
 #pragma unroll
         for (int k = 0; k < 4; ++k)
             st.c[4 * b + k] = *reinterpret_cast<const uint4*>(cp + (uint64_t)b * (kWave * kBlkSteps) + 4 * k);
-    // query: 32 bytes from the aligned piece holding row 16h
-    const uint8_t* qb = (const uint8_t*)((uintptr_t)Q & ~(uintptr_t)15);
-    const uint32_t qm = (uint32_t)(uintptr_t)Q & 15u;
-    const uint32_t qo = (qm + 16u * (uint32_t)h) & ~15u, qhi = (qm + n - 1u) & ~15u;
-    qmis = (qm + 16u * (uint32_t)h) & 15u;
-    st.q[0] = *reinterpret_cast<const uint4*>(qb + min(qo, qhi));
-    st.q[1] = *reinterpret_cast<const uint4*>(qb + min(qo + 16u, qhi));
     // target: 80 bytes from the aligned piece holding the window's first column
-    const uint8_t* tb = (const uint8_t*)((uintptr_t)T & ~(uintptr_t)15);
     const int tm = (int)((uint32_t)(uintptr_t)T & 15u);
+    const uint8_t* tb = T - tm;
     const int cw = 16 * u0 - (int)ln;  // the window's first column
     const int thi = (tm + (int)m - 1) & ~15;
     const int to = (tm + cw) & ~15;  // (floor; pieces outside the pair hold clamped copies, never read)
 #pragma unroll
-    for (int k = 0; k < 5; ++k) st.t[k] = *reinterpret_cast<const uint4*>(tb + min(max(to + 16 * k, 0), thi));
+    for (int k = 0; k < kBwTPieces; ++k) bw_dma16(tb + min(max(to + 16 * k, 0), thi), stage + (2u + k) * (kWave * 16u));
     // ring positions follow the unclamped pieces' addresses
     ta16 = (uint32_t)(uintptr_t)tb + (uint32_t)to;
+    // query: 32 bytes from the aligned piece holding row 16h
+    // (pointer arithmetic from Q and T, not integer casts: keeps the loads global, not flat)
+    const uint32_t qm = (uint32_t)(uintptr_t)Q & 15u;
+    const uint8_t* qb = Q - qm;
+    const uint32_t qo = (qm + 16u * (uint32_t)h) & ~15u, qhi = (qm + n - 1u) & ~15u;
+    qmis = (qm + 16u * (uint32_t)h) & 15u;
+    bw_dma16(qb + min(qo, qhi), stage);
+    bw_dma16(qb + min(qo + 16u, qhi), stage + kWave * 16u);
     return 16 * u0;
 }
 
 // The staged stripe into its slot: codes at step & 63, target bytes at their
 // address & 127, the 16 query bytes shifted to the slot's query field, and the
 // header (stripe, first step) that tells a step whether its cell is inside.
-__device__ __forceinline__ void bw_commit(const BwStage& st, uint32_t sb, uint32_t qmis, uint32_t ta16, int h,
-                                          int w0) {
+__device__ __forceinline__ void bw_commit(const BwStage& st, uint32_t stl, uint32_t sb, uint32_t qmis, uint32_t ta16,
+                                          int h, int w0) {
+    // (stl: this lane's pieces in the LDS-DMA stage; every DMA of the round has landed)
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    uint4 tq[kBwStagePieces];
 #pragma unroll
-    for (int k = 0; k < 16; ++k) lds_st128(sb + ((uint32_t)(w0 * 4 + 16 * k) & 255u), st.c[k]);
+    for (int k = 0; k < kBwStagePieces; ++k) tq[k] = lds_ld128(stl + (uint32_t)k * (kWave * 16u));
 #pragma unroll
-    for (int k = 0; k < 5; ++k) lds_st128(sb + kBwT + ((ta16 + 16u * k) & 127u), st.t[k]);
-    const uint32_t w[8] = {st.q[0].x, st.q[0].y, st.q[0].z, st.q[0].w, st.q[1].x, st.q[1].y, st.q[1].z, st.q[1].w};
+    for (int k = 0; k < 4 * kBwBlocks; ++k) lds_st128(sb + ((uint32_t)(w0 * 4 + 16 * k) & 255u), st.c[k]);
+#pragma unroll
+    for (int k = 0; k < kBwTPieces; ++k) lds_st128(sb + kBwT + ((ta16 + 16u * k) & 127u), tq[2 + k]);
+    const uint32_t w[8] = {tq[0].x, tq[0].y, tq[0].z, tq[0].w, tq[1].x, tq[1].y, tq[1].z, tq[1].w};
     const uint32_t a = qmis >> 2, sh = qmis & 3u;
     uint32_t s[5];
 #pragma unroll
@@ -196,22 +221,22 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const uint32_t reg = lds_addr(lds) + (uint32_t)lane * kBwRegion;
     const uint32_t rl = reg + kBwRuns;  // event list: 64 entries, two halves of 32
+    const uint32_t stage = lds_addr(lds) + kWave * kBwRegion, stl = stage + 16u * (uint32_t)lane;
     const uint32_t tlow = (uint32_t)(uintptr_t)T;  // target byte c lives at ring (tlow + c) & 127
     bool live = has && H > 0;           // a positive score has its goal at i, j >= 1
     int g = live ? (int)((gi - 1u) >> 4) : 0, r = live ? (int)((gi - 1u) & 15u) : 0, c = live ? (int)gj - 1 : 0;
     // every slot's header invalid (stripe -1)
 #pragma unroll
     for (int s = 0; s < kBwSlots; ++s) lds_st64(reg + s * kBwSlotB + kBwHdr, -1, 0);
-    BwStage st;
-    uint32_t qmis = 0, ta16 = 0;
     // the goal's stripe, staged at once
     if (live) {
-        const int w0 = bw_issue(st, P, Q, T, n, m, nb, g, c - r + 8, qmis, ta16);
-        bw_commit(st, reg + ((uint32_t)g & 3u) * kBwSlotB, qmis, ta16, g, w0);
+        BwStage st;
+        uint32_t qmis = 0, ta16 = 0;
+        const int w0 = bw_issue(st, stage, P, Q, T, n, m, nb, g, c - r + 8, qmis, ta16);
+        bw_commit(st, stl, reg + ((uint32_t)g & 3u) * kBwSlotB, qmis, ta16, g, w0);
     }
     int lo = g;                 // lowest stripe staged or in flight
-    bool pend = false, stalled = false;
-    int pend_h = 0, pend_w0 = 0;
+    bool stalled = false;
     uint32_t nr = 0u, nout = 0u;  // events listed, events in HBM
 #ifdef TA_BW_PROF
     uint64_t bwp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -221,15 +246,9 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
     asm volatile("" : "+v"(mav), "+v"(miv), "+v"(gapv));
     BW_T(t_begin);
     while (ballot(live)) {
-        // ---- staging round: commit what the last round loaded, issue the next stripe
-        BW_T(t0);
-        if (pend) {
-            bw_commit(st, reg + ((uint32_t)pend_h & 3u) * kBwSlotB, qmis, ta16, pend_h, pend_w0);
-            pend = false;
-            if (pend_h == g) stalled = false;
-        }
+        // ---- staging round: issue the next stripe's loads (they land while this
+        // round's walk iterations run), commit them at the round's end
         BW_T(t1);
-        BW_ACC(0, t1 - t0);
         int h = -1, ctr = 0;
         if (live) {
             if (stalled) {  // the walk left its window: restage its stripe around the current cell
@@ -240,13 +259,15 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
                 ctr = c - r + 8 - 16 * (g - h);
             }
         }
-        if (h >= 0) {
-            pend_w0 = bw_issue(st, P, Q, T, n, m, nb, h, ctr, qmis, ta16);
-            pend_h = h;
-            pend = true;
+        BwStage st;
+        uint32_t qmis = 0, ta16 = 0;
+        int pend_w0 = 0;
+        const bool pend = h >= 0;
+        if (pend) {
+            pend_w0 = bw_issue(st, stage, P, Q, T, n, m, nb, h, ctr, qmis, ta16);
             lo = min(lo, h);
         }
-        // a full half of the event list to HBM (at most 8 events per round)
+        // a full half of the event list to HBM (at most TA_BW_EVENTS events per round)
         if (nr - nout >= 32u) {
             bw_runs_out(rl + ((nout & 32u) << 2), rout + nout);
             nout += 32u;
@@ -254,14 +275,15 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
         BW_T(t2);
         BW_ACC(1, t2 - t1);
         BW_ACC(5, 1);
-        // ---- walk iterations, branch-free: every lane computes both columns and
-        // writes both events (an event past the count is overwritten later; the
-        // list never holds more than 39 pending), and only the lanes whose cell
-        // is inside their staged window keep the results.  The LDS reads of a
-        // step go out together; a walk that leaves its window stops there until
-        // its stripe is restaged.  With kBwCols = 2 a step also reads the next
-        // column's code and target byte and, when the first move stays in the
-        // stripe, makes the second move too.
+        // ---- walk iterations, branch-free: every lane computes all kBwCols
+        // columns and writes all their events (an event past the count is
+        // overwritten later; the list never holds more than 50 pending), and only
+        // the lanes whose cell is inside their staged window keep the results.
+        // The LDS reads of a step go out together: the codes and target bytes of
+        // columns c .. c - kBwCols + 1; column k is walked when column k - 1's
+        // move stayed in the stripe (an M or I move: the next cell is in column
+        // c - k), the walk goes on and step t - k is inside the window.  A walk
+        // that leaves its window stops there until its stripe is restaged.
 #pragma unroll
         for (int it = 0; it < kBwRound; ++it) {
 #ifdef TA_BW_PROF
@@ -270,19 +292,19 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
 #endif
             const uint32_t ln = (uint32_t)g & 63u, t = (uint32_t)c + ln;
             const uint32_t sb = reg + (((uint32_t)g & 3u) << 9);
-            const uint32_t tr = sb + kBwT;
+            const uint32_t tr = sb + kBwT, tc = tlow + (uint32_t)c;
             bw_v2 hd = lds_ld64(sb + kBwHdr);
-            uint32_t x = lds_ld32(sb + ((t & 63u) << 2));
             uint4 q4 = lds_ld128(sb + kBwQ);
-            uint32_t tb = lds_ld8(tr + ((tlow + (uint32_t)c) & 127u));
-            uint32_t x1 = 0, tb1 = 0;
-            if constexpr (kBwCols == 2) {
-                x1 = lds_ld32(sb + (((t - 1u) & 63u) << 2));
-                tb1 = lds_ld8(tr + ((tlow + (uint32_t)c - 1u) & 127u));
+            uint32_t xs[kBwCols], tbs[kBwCols];
+#pragma unroll
+            for (int k = 0; k < kBwCols; ++k) {
+                xs[k] = lds_ld32(sb + (((t - (uint32_t)k) & 63u) << 2));
+                tbs[k] = lds_ld8(tr + ((tc - (uint32_t)k) & 127u));
             }
             // (keeps the reads together ahead of their uses)
-            asm volatile("" : "+v"(hd), "+v"(x), "+v"(q4.x), "+v"(q4.y), "+v"(q4.z), "+v"(q4.w), "+v"(tb), "+v"(x1),
-                         "+v"(tb1));
+            asm volatile("" : "+v"(hd), "+v"(q4.x), "+v"(q4.y), "+v"(q4.z), "+v"(q4.w));
+#pragma unroll
+            for (int k = 0; k < kBwCols; ++k) asm volatile("" : "+v"(xs[k]), "+v"(tbs[k]));
             const bool inwin = (int)hd.x == g && t - hd.y < (uint32_t)kBwWin;
             const bool ok = live && !stalled && inwin;
             stalled = stalled || (live && !inwin);
@@ -308,41 +330,42 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
                 ev = ((uint32_t)kd << 2) | (top ? 3u : ib);
                 nrow = (top || ib) ? rp : rp - 1;
             };
-            int dH1, nrow1;
-            uint32_t ev1;
-            bool top1;
-            column(x, tb, r, dH1, ev1, nrow1, top1);
-            lds_st32(rl + ((nr & 63u) << 2), ev1);
-            const int H1 = H - dH1;
-            if constexpr (kBwCols == 2) {
-                // the second column: the move stayed in the stripe, the walk goes on,
-                // and column c - 1 is inside the window
-                int dH2, nrow2;
-                uint32_t ev2;
-                bool top2;
-                column(x1, tb1, nrow1 & 15, dH2, ev2, nrow2, top2);
-                lds_st32(rl + (((nr + 1u) & 63u) << 2), ev2);
-                const bool two = ok && !top1 && nrow1 >= 0 && H1 > 0 && t - 1u - hd.y < (uint32_t)kBwWin;
-                const int dc = (top1 ? 0 : 1) + ((two && !top2) ? 1 : 0);
-                const int nrowf = two ? nrow2 : nrow1;
-                const int Hf = two ? H1 - dH2 : H1;
-                c -= ok ? dc : 0;
-                H = ok ? Hf : H;
-                nr += (ok ? 1u : 0u) + (two ? 1u : 0u);
-                // the next cell: up the stripe (D run), left (I) or diagonal (M)
-                g += ok ? (nrowf >> 31) : 0;  // -1 when the row leaves the stripe's top
-                r = ok ? (nrowf & 15) : r;    // (-1 -> 15)
-            } else {
-                c -= (ok && !top1) ? 1 : 0;
-                H = ok ? H1 : H;
-                nr += ok ? 1u : 0u;
-                g += ok ? (nrow1 >> 31) : 0;
-                r = ok ? (nrow1 & 15) : r;
+            bool take = ok, prev_top = false;
+            int rr = r, Hc = H, nrowf = 0, dc = 0;
+            uint32_t ne = 0u;
+#pragma unroll
+            for (int k = 0; k < kBwCols; ++k) {
+                int dH, nrow;
+                uint32_t ev;
+                bool top;
+                column(xs[k], tbs[k], rr & 15, dH, ev, nrow, top);
+                lds_st32(rl + (((nr + (uint32_t)k) & 63u) << 2), ev);
+                if (k > 0) take = take && !prev_top && rr >= 0 && Hc > 0 && t - (uint32_t)k - hd.y < (uint32_t)kBwWin;
+                Hc = take ? Hc - dH : Hc;
+                ne += take ? 1u : 0u;
+                dc += (take && !top) ? 1 : 0;
+                nrowf = take ? nrow : nrowf;
+                prev_top = top;
+                rr = nrow;
             }
+            // the next cell: up the stripe (D run), left (I) or diagonal (M)
+            c -= dc;
+            H = Hc;
+            nr += ne;
+            g += ok ? (nrowf >> 31) : 0;  // -1 when the row leaves the stripe's top
+            r = ok ? (nrowf & 15) : r;    // (-1 -> 15)
             live = live && H > 0;
         }
         BW_T(t3);
         BW_ACC(3, t3 - t2);
+        // ---- the stripe loaded this round into its slot (the walk reads it from
+        // the next round on); a stalled walk whose stripe this is goes on
+        if (pend) {
+            bw_commit(st, stl, reg + ((uint32_t)h & 3u) * kBwSlotB, qmis, ta16, h, pend_w0);
+            if (h == g) stalled = false;
+        }
+        BW_T(t4);
+        BW_ACC(0, t4 - t3);
     }
     BW_T(t_end);
     BW_ACC(4, t_end - t_begin);
@@ -358,6 +381,32 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
         for (uint32_t j = nout; j < nr; ++j) rout[j] = lds_ld32(rl + ((j & 63u) << 2));
         a.cigar_len[p] = nr;  // the event count, for format_runs_kernel
     }
+}
+
+// Wave-wide inclusive scans in DPP (row_shr 1, 2, 4, 8 within each 16-lane row,
+// then row_bcast 15 / 31 across rows): six VALU ops where __shfl_up steps are
+// six ds_bpermute round trips.  Lanes without a source add 0 (max: INT_MIN).
+__device__ __forceinline__ uint32_t bw_scan_add(uint32_t v) {
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118, 0xF, 0xF, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142, 0xA, 0xF, false);  // row_bcast:15 -> rows 1, 3
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143, 0xC, 0xF, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+__device__ __forceinline__ int bw_scan_max(int v) {
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x111, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x112, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x114, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x118, 0xF, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x142, 0xA, 0xF, false));
+    v = max(v, __builtin_amdgcn_update_dpp(INT_MIN, v, 0x143, 0xC, 0xF, false));
+    return v;
+}
+// lane l gets lane l + 1's v (lane 63: last63)
+__device__ __forceinline__ int wave_shl1(int last63, int v) {
+    return __builtin_amdgcn_update_dpp(last63, v, 0x130, 0xF, 0xF, false);
 }
 
 // Decimal digits of c (c < 2^32).
@@ -419,33 +468,23 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
         const bool va = kd > 0, vb = mop != 3u;      // item A: D x kd; item B: the move (M / I) x 1
         const uint32_t first = va ? 2u : mop;        // op of the event's first / last item (3: no item)
         const uint32_t last = vb ? mop : (va ? 2u : 3u);
-        // the previous event's last op (lane 0: the carried run's).  The shuffle
-        // stays outside the select: inside `?:` it becomes a branch that masks
-        // lane 0 off, and a bpermute reads 0 from a masked-off lane.
-        const uint32_t lup = (uint32_t)__shfl_up((int)last, 1, 64);
-        const uint32_t plast = lane == 0 ? cop : lup;
-        const uint32_t nfirst = (uint32_t)__shfl_down((int)first, 1, 64);  // (lane 63: unknown)
+        // the previous event's last op (lane 0: the carried run's), the next
+        // event's first (lane 63: unused).  (Cross-lane moves stay out of any
+        // select: inside `?:` one becomes a branch that masks lanes off, and a
+        // masked-off source lane reads as 0.)
+        const uint32_t plast = (uint32_t)wave_shr1((int)cop, (int)last);
+        const uint32_t nfirst = (uint32_t)wave_shl1(3, (int)first);
         const bool ha = va && plast != 2u;                   // A starts a run
         const bool hb = vb && (va || plast != mop);          // B starts a run (always after an A)
         // item prefix sums: lane k's items end at pre_k; the carried count precedes lane 0
         const uint32_t tot = kd + (vb ? 1u : 0u);
-        uint32_t pre = tot + (lane == 0 ? ccnt : 0u);
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
-            if (lane >= o) pre += y;
-        }
+        const uint32_t pre = bw_scan_add(tot + (lane == 0 ? ccnt : 0u));
         const uint32_t preA = pre - (vb ? 1u : 0u);  // through item A
         // the prefix just before the latest run head at or before each lane's end
         // (a max scan: prefixes grow); the carried run's head sits at prefix 0
         int hv = hb ? (int)(pre - 1u) : (ha ? (int)(preA - kd) : -1);
-        int hmax = hv;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const int y = __shfl_up(hmax, o, 64);
-            if (lane >= o) hmax = max(hmax, y);
-        }
-        const int hprev0 = __shfl_up(hmax, 1, 64);
+        const int hmax = bw_scan_max(hv);
+        const int hprev0 = wave_shr1(0, hmax);
         const int hprev = lane == 0 ? 0 : max(hprev0, 0);  // (lane 0 continues the carry: head at 0)
         const uint32_t sumA = preA - (uint32_t)(ha ? (int)(preA - kd) : hprev);
         const uint32_t sumB = pre - (uint32_t)(hb ? (int)(pre - 1u) : hprev);
@@ -457,14 +496,9 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
         const bool eb = act && vb && !more && nxt_diff;
         const uint32_t dA = bw_digits(sumA), dB = bw_digits(sumB);
         const uint32_t LA = ea ? dA + 1u : 0u, LB = eb ? dB + 1u : 0u;
-        uint32_t incl = LA + LB;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)incl, o, 64);
-            if (lane >= o) incl += y;
-        }
+        const uint32_t incl = bw_scan_add(LA + LB);
         // the carried run, when lane 0's first item does not continue it, ends first
-        const uint32_t f0 = (uint32_t)__shfl((int)first, 0, 64);
+        const uint32_t f0 = (uint32_t)__builtin_amdgcn_readlane((int)first, 0);
         if (cop != 3u && f0 != cop) {
             const uint32_t dg = bw_digits(ccnt);
             bw_put_run(end - used - (dg + 1u), ccnt, cop, dg, lane == 0);
@@ -474,11 +508,11 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
         char* q = end - used - incl;
         bw_put_run(q, sumB, mop, dB, eb);
         bw_put_run(q + LB, sumA, 2u, dA, ea);
-        used += (uint32_t)__shfl((int)incl, 63, 64);
+        used += (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
         // carry lane 63's open run into the next round
         const bool cont = base + 64u < E;
-        const uint32_t l63 = (uint32_t)__shfl((int)last, 63, 64);
-        const uint32_t s63 = (uint32_t)__shfl((int)(vb ? sumB : sumA), 63, 64);
+        const uint32_t l63 = (uint32_t)__builtin_amdgcn_readlane((int)last, 63);
+        const uint32_t s63 = (uint32_t)__builtin_amdgcn_readlane((int)(vb ? sumB : sumA), 63);
         cop = cont ? l63 : 3u;
         ccnt = cont ? s63 : 0u;
     }
