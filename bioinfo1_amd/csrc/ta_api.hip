@@ -319,14 +319,9 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
             // fill handed back ('-' bytes) in the one-pair walk: its list and count
             t.pflag = pl->d_pflag;
             t.runs = static_cast<uint32_t*>(ctx->ws_runs.p);
+            t.fb_order = pl->d_fb + 2ull * ch.cbegin;
+            t.fb_count = pl->d_fb + h.n_dual_pairs + c;
             TA_HIP(ctx, ta::launch_traceback(h.type, t, s, 64));
-            ta::TraceArgs f = t;
-            f.order = pl->d_fb + 2ull * ch.cbegin;
-            f.begin = 0;
-            f.count = 2 * (ch.dcount + ch.fcount);
-            f.count_dev = pl->d_fb + h.n_dual_pairs + c;
-            f.pflag = nullptr;
-            TA_HIP(ctx, ta::launch_traceback(h.type, f, s, 0));
         } else {
             TA_HIP(ctx, ta::launch_traceback(h.type, t, s, h.walk_group));
         }

@@ -33,12 +33,14 @@ struct DualOut {
     PassOut o[2];
 };
 
-// BLK: steps staged in LDS between flushes (16: 8 KB per wave; 8: 4 KB, half-block stores)
+// BLK: steps staged in LDS between flushes (16: 8 KB per wave; 8: 4 KB, half-block stores;
+// 0: no staging, one scattered dword store per step and pair, merged in L2)
 #ifndef TA_DUAL_STAGE
 #define TA_DUAL_STAGE 16
 #endif
 constexpr int kDualStage = TA_DUAL_STAGE;
-static_assert(kDualStage == 8 || kDualStage == 16, "dual BLK staging");
+static_assert(kDualStage == 0 || kDualStage == 8 || kDualStage == 16, "dual BLK staging");
+constexpr int kDualStageL = kDualStage ? kDualStage : 16;  // (array sizes and masks when staged)
 
 struct DualIo {
     const uint8_t* Q[2];
@@ -173,13 +175,13 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // BLK: the staged kDualStage steps ending at step t (inclusive) -> their
     // place in block t / 16, [b][lane][16], of both pairs
     auto blk_flush = [&](uint32_t t) {
-        const uint64_t at = ((uint64_t)(t >> 4) * kWave + (uint32_t)lane) * kBlkSteps + (t & 15u & ~(uint32_t)(kDualStage - 1));
+        const uint64_t at = ((uint64_t)(t >> 4) * kWave + (uint32_t)lane) * kBlkSteps + (t & 15u & ~(uint32_t)(kDualStageL - 1));
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             uint32_t* dst = (h ? prow1 : prow0) + at;
-            const uint32_t* src = io.cbuf + h * (kDualStage * kWave) + lane;
+            const uint32_t* src = io.cbuf + h * (kDualStageL * kWave) + lane;
 #pragma unroll
-            for (int q = 0; q < kDualStage / 4; ++q) {
+            for (int q = 0; q < kDualStageL / 4; ++q) {
                 // (one 16-byte piece at a time: the step loop's registers are all live here)
                 __builtin_amdgcn_sched_barrier(0);
                 uint4 v;
@@ -321,9 +323,15 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             const uint32_t cA = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
             const uint32_t cB = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
             if constexpr (BLK) {
-                const uint32_t sl = (t & (uint32_t)(kDualStage - 1)) * kWave + (uint32_t)lane;
-                io.cbuf[sl] = cA;
-                io.cbuf[kDualStage * kWave + sl] = cB;  // (flushed by run_steps)
+                if constexpr (kDualStage == 0) {
+                    const uint32_t off = (uint32_t)blk_index(0, t, (uint32_t)lane, io.nb);  // (within the pass)
+                    prow0[off] = cA;
+                    prow1[off] = cB;
+                } else {
+                    const uint32_t sl = (t & (uint32_t)(kDualStage - 1)) * kWave + (uint32_t)lane;
+                    io.cbuf[sl] = cA;
+                    io.cbuf[kDualStage * kWave + sl] = cB;  // (flushed by run_steps)
+                }
             } else {
                 // 32-bit byte offset from the uniform row base (SGPR base + VGPR offset stores)
                 const uint32_t off = (t * kWave + (uint32_t)lane) * 4u;
@@ -345,14 +353,14 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             uint32_t blk = min(t_end, next_reload);
             // BLK: stop at each 16-step block end, flushing outside the step body
             // (a branch inside it costs the whole step loop spills)
-            if constexpr (BLK) blk = min(blk, (t | (uint32_t)(kDualStage - 1)) + 1u);
+            if constexpr (BLK && kDualStage) blk = min(blk, (t | (uint32_t)(kDualStage - 1)) + 1u);
             for (; t + 1 < blk; t += 2) {
                 step(t, masked_tag);
                 step(t + 1, masked_tag);
             }
             if (t < blk) step(t++, masked_tag);
-            if constexpr (BLK)
-                if ((t & (uint32_t)(kDualStage - 1)) == 0 || t == steps) blk_flush(t - 1);
+            if constexpr (BLK && kDualStage)
+                if ((t & (uint32_t)(kDualStageL - 1)) == 0 || t == steps) blk_flush(t - 1);
         }
     };
     run_steps(ramp_end, std::true_type{});
@@ -460,7 +468,7 @@ template <int MODE, bool CIGAR, bool BLK = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
     // BLK: code staging per wave (kDualStage steps x 64 lanes x 2 pairs)
-    __shared__ uint32_t cbuf_all[BLK ? kWavesPerBlock * 2 * kDualStage * kWave : 1];
+    __shared__ uint32_t cbuf_all[(BLK && kDualStage) ? kWavesPerBlock * 2 * kDualStage * kWave : 1];
     uint32_t widx, p_only = 0;
     const bool pipe = a.ticket != nullptr;
     if (pipe) {
@@ -491,7 +499,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     io.rec_r = nullptr;
     io.tag_w = io.tag_r = 0;
     io.err = a.err;
-    io.cbuf = cbuf_all + (BLK ? (threadIdx.x >> 6) * (2 * kDualStage * kWave) : 0);
+    io.cbuf = cbuf_all + ((BLK && kDualStage) ? (threadIdx.x >> 6) * (2 * kDualStage * kWave) : 0);
     io.nb = blk_count(m);
     bool dash = false, qother = false;
 #pragma unroll

@@ -927,7 +927,27 @@ __global__ __launch_bounds__(kWave) void traceback_lane_kernel(TraceArgs a) {
 // block (ta_walk_band.h).
 __global__ __launch_bounds__(kWave) __attribute__((amdgpu_waves_per_eu(1, 1))) void traceback_band_kernel(TraceArgs a) {
     __shared__ __attribute__((aligned(16))) uint8_t lds[kWave * kBwRegion + kBwStageBytes];
-    traceback_band_local(a, lds, (int)threadIdx.x);
+    const int lane = (int)threadIdx.x;
+    traceback_band_local(a, lds, lane);
+    // then the pairs the dual fill handed back ('-' bytes; usually none), one
+    // wave per pair in the one-pair walk over the blocked layout -- here rather
+    // than in a launch of its own, whose count only the device knows
+    if (a.fb_count) {
+        const uint32_t nfb = *a.fb_count;
+        for (uint32_t w = blockIdx.x; w < nfb; w += gridDim.x) {
+            const uint32_t p = a.fb_order[w];
+            const uint32_t n = a.qlen[p], m = a.tlen[p];
+            uint64_t st;
+            uint32_t len;
+            const WalkSeq seq{a.qbytes + a.qoff[p], a.tbytes + a.toff[p], a.score[p], a.match, a.mismatch, a.gap};
+            traceback_pair<kLocal>(a.ptrs + a.ptr_off[p], n, m, a.goal_i[p], a.goal_j[p], a.slots + a.slot_off[p],
+                                   cigar_slot_bytes(n, m), lane, &st, &len, seq, true);
+            if (lane == 0) {
+                a.cigar_start[p] = a.slot_off[p] + st;
+                a.cigar_len[p] = len;
+            }
+        }
+    }
 }
 
 // ... and their runs into CIGAR text, one wave per pair.

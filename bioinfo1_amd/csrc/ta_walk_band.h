@@ -331,7 +331,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
                 nrow = (top || ib) ? rp : rp - 1;
             };
             bool take = ok, prev_top = false;
-            int rr = r, Hc = H, nrowf = 0, dc = 0;
+            int rr = r, Hc = H, nrowf = r, dc = 0;  // (no column taken: the cell stays)
             uint32_t ne = 0u;
 #pragma unroll
             for (int k = 0; k < kBwCols; ++k) {
@@ -352,8 +352,8 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
             c -= dc;
             H = Hc;
             nr += ne;
-            g += ok ? (nrowf >> 31) : 0;  // -1 when the row leaves the stripe's top
-            r = ok ? (nrowf & 15) : r;    // (-1 -> 15)
+            g += nrowf >> 31;  // -1 when the row leaves the stripe's top
+            r = nrowf & 15;    // (-1 -> 15)
             live = live && H > 0;
         }
         BW_T(t3);
