@@ -317,7 +317,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
                 const int kd = (int)__builtin_ctz(~dp);  // <= rr + 1
                 const int rp = rr - kd;
                 top = rp < 0;
-                const uint32_t ib = (xc >> ((uint32_t)(15 - rp) & 31u)) & 1u;
+                const uint32_t ib = __builtin_amdgcn_ubfe(xc, (uint32_t)(15 - rp), 1u);  // (offset mod 32)
                 const uint32_t sel = (uint32_t)rp & 7u;
                 const uint32_t qlo = __builtin_amdgcn_perm(q4.y, q4.x, sel), qhi = __builtin_amdgcn_perm(q4.w, q4.z, sel);
                 uint32_t qb = ((rp & 8) ? qhi : qlo) & 0xFFu;
