@@ -314,7 +314,7 @@ class Server:
 
     def last_times(self, slot: int = 0):
         """Device phase times (us) of slot's last request: request + bytes to HBM,
-        fill + walk, results out, system fence."""
+        fill + walk, results out, 0 (the release store of `done` is the fence)."""
         out = (C.c_double * 4)()
         r = lib().ta_server_last_times(self._h, slot, out)
         if r != TA_OK:

@@ -98,14 +98,15 @@ int ta_server_pause(ta_server* server);
 int ta_server_resume(ta_server* server);
 /* Diagnostics: the device-side phase times (microseconds) of the last request
  * served in `slot`: [0] request + bytes into HBM, [1] fill + walk, [2] results
- * and CIGAR into the slot, [3] the system-scope release fence. */
+ * and CIGAR into the slot, [3] 0 (the release store of `done` is the fence). */
 int ta_server_last_times(const ta_server* server, uint32_t slot, double* us_out4);
 
 /* The drop-in team::Align (include/team_alignment.hpp) runs each call on:
  * the device set here (device >= 0; -1 clears the choice), else the device
  * named by the TEAM_ALIGN_DEVICE environment variable (read once), else the
- * calling thread's current HIP device (hipSetDevice).  TA_ERR_ARG for a device
- * that does not exist. */
+ * calling thread's current HIP device (hipSetDevice) as of that thread's first
+ * call (a thread keeps it: hipGetDevice per call would cost more than a small
+ * pair's alignment).  TA_ERR_ARG for a device that does not exist. */
 int ta_set_default_device(int device);
 /* The calling thread's current HIP device (0 when it has none) and the number of devices. */
 int ta_current_device(void);
