@@ -94,7 +94,6 @@ struct TraceArgs {
     int match, mismatch, gap;
     uint32_t blk;                // codes in the blocked layout (ta_layout.h blk_index)
     const uint8_t* pflag;        // band walk: pairs to leave to the fallback walk (FillArgs.pflag)
-    const uint32_t* count_dev;   // non-null: pair count read on the device (the hand-back list)
     uint32_t* runs;              // band walks: run words, pair p's at runs + slot_off[p] / 2 (format_runs_kernel)
     const uint32_t* fb_order;    // band walks: the dual fill's hand-back list ('-' couples), walked after the band
     const uint32_t* fb_count;    // ... and its length (on the device)

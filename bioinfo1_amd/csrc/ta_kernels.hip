@@ -892,8 +892,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_TB_WP
     // Wave-strided over the pairs (one wave per pair: the grid covers them all).
     const int lane = threadIdx.x & 63;
     const uint32_t stride = gridDim.x * kWavesPerBlock;
-    const uint32_t count = a.count_dev ? *a.count_dev : a.count;  // (the band walk's fallback: the hand-back list)
-    for (uint32_t widx = wave_id(); widx < count; widx += stride) {
+    for (uint32_t widx = wave_id(); widx < a.count; widx += stride) {
         const uint32_t p = a.order ? a.order[a.begin + widx] : a.begin + widx;
         const uint32_t n = a.qlen[p], m = a.tlen[p];
         uint64_t st;
@@ -1059,16 +1058,6 @@ hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int gro
     if (mode == kLocal && group == 64) {  // band walks (blocked layout), one lane per pair
         hipLaunchKernelGGL(traceback_band_kernel, dim3((a.count + kWave - 1) / kWave), dim3(kWave), 0, s, a);
         hipLaunchKernelGGL(format_runs_kernel, g, b, 0, s, a);
-        return hipGetLastError();
-    }
-    if (a.count_dev) {  // the band walk's fallback (the hand-back list, count on the device): capped grid
-        const dim3 gc((std::min<uint32_t>(a.count, 1024u) + kWavesPerBlock - 1) / kWavesPerBlock);
-        switch (mode) {
-            case kGlobal: hipLaunchKernelGGL(traceback_kernel<kGlobal>, gc, b, 0, s, a); break;
-            case kLocal: hipLaunchKernelGGL(traceback_kernel<kLocal>, gc, b, 0, s, a); break;
-            case kSemi: hipLaunchKernelGGL(traceback_kernel<kSemi>, gc, b, 0, s, a); break;
-            default: return hipErrorInvalidValue;
-        }
         return hipGetLastError();
     }
     if (mode == kLocal && group == 16) {  // lane walks (TA_LW_G lanes per pair)
