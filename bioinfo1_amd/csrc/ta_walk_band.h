@@ -354,7 +354,9 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
             nr += ne;
             g += nrowf >> 31;  // -1 when the row leaves the stripe's top
             r = nrowf & 15;    // (-1 -> 15)
-            live = live && H > 0;
+            // (events of a walk <= its columns + stripe crossings <= m + n/16 + 1: the
+            // cap never binds on a correct walk; it bounds the list and the loop)
+            live = live && H > 0 && nr + kBwCols <= n + m + 1u;
         }
         BW_T(t3);
         BW_ACC(3, t3 - t2);
