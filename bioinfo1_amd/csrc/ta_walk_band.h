@@ -13,23 +13,26 @@
 // gap move never lowers the cost, so the walk can only end right after a
 // diagonal move.
 //
-// One iteration resolves the D run above the current cell inside its stripe
-// from ONE code dword (the D plane shifted so that the current row is bit 0:
-// trailing ones), then the M or I move at the row the run stops on.  A walk
-// follows its stripe (16 rows) along the steps, which in the blocked layout are
-// contiguous: a stripe's 64-step window is 4 x 64 bytes.  Each walker stages
-// the windows of the stripes ahead of it -- predicted along the diagonal from
-// its current cell -- into a ring of 4 slots (stripe & 3).  A slot is
-// addressed by position alone (codes at step & 63, target bytes at their
-// address & 127), and carries its stripe and window start in a header read
-// beside the data, so a step needs no per-slot bookkeeping in registers.
-// Staging runs in rounds: every kBwRound iterations all lanes write the
-// registers they loaded in the previous round into their slot (the loads had a
-// whole round to land) and issue the loads of the next stripe, so no walker
-// waits on memory unless its path left its predicted window (it then sits out
-// until its stripe is restaged around its actual cell).  Runs go to an LDS list
-// per walker, leave for HBM 16 at a time, and format_runs_kernel turns them
-// into the CIGAR text (the RunWriter layout, ta_device.h).
+// A column resolves the D run above the current cell inside its stripe from
+// ONE code dword (the D plane shifted so that the current row is bit 0:
+// trailing ones), then the M or I move at the row the run stops on; an
+// iteration reads kBwCols columns' operands in one batch of LDS reads and walks
+// them while the moves stay in the stripe.  A walk follows its stripe (16 rows)
+// along the steps, which in the blocked layout are contiguous: a stripe's
+// 64-step window is 4 x 64 bytes.  Each walker stages the windows of the
+// stripes ahead of it -- predicted along the diagonal from its current cell --
+// into a ring of 4 slots (stripe & 3).  A slot is addressed by position alone
+// (codes at step & 63, target bytes at their address & 127), and carries its
+// stripe and window start in a header read beside the data, so a step needs no
+// per-slot bookkeeping in registers.  Staging runs in rounds of kBwRound
+// iterations: a round issues the next stripe's loads (codes into registers,
+// query and target pieces by LDS-DMA), walks, and commits the stripe to its
+// slot at its end, so no walker waits on memory unless its path left its
+// predicted window (it then sits out until its stripe is restaged around its
+// actual cell).  Every walked column leaves an event (D-run length, move) in an
+// LDS list per walker that goes to HBM 32 at a time; format_runs_kernel merges
+// the events into runs and writes the CIGAR text (the RunWriter layout,
+// ta_device.h).
 #pragma once
 
 #include "ta_walk_lane.h"
