@@ -66,10 +66,14 @@ constexpr int kBwRunCap = 64;                     // event list: two halves of 3
 #endif
 constexpr int kBwCols = TA_BW_COLS;               // columns a walk iteration may move (1, 2 or 4)
 #ifndef TA_BW_EVENTS
-#define TA_BW_EVENTS 16
+#define TA_BW_EVENTS 12
 #endif
 constexpr int kBwRound = TA_BW_EVENTS / kBwCols;  // walk iterations per staging round (<= 16 events)
-constexpr int kBwLook = 3;                        // stripes staged ahead of the walk
+#ifndef TA_BW_LOOK
+#define TA_BW_LOOK 3
+#endif
+constexpr int kBwLook = TA_BW_LOOK;               // stripes staged ahead of the walk (<= kBwSlots - 1)
+static_assert(kBwLook >= 1 && kBwLook < kBwSlots, "band walk lookahead");
 constexpr int kBwRuns = kBwSlots * kBwSlotB;      // region offset of the run list
 constexpr int kBwRegion = kBwRuns + kBwRunCap * 4 + 16;  // 2320 = 580 dwords (4 mod 32: spreads banks)
 static_assert(kBwRegion % 16 == 0 && kBwHdr + 8 <= kBwSlotB, "band walk LDS layout");
