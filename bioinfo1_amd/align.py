@@ -80,6 +80,7 @@ def lib() -> C.CDLL:
     L.ta_context_held_bytes.argtypes = [C.c_void_p]
     L.ta_context_held_bytes.restype = C.c_uint64
     L.ta_set_default_device.argtypes = [C.c_int]
+    L.ta_set_thread_device.argtypes = [C.c_int]
     L.ta_plan_create.argtypes = [C.c_void_p, C.c_uint32, u32p, u32p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int,
                                  C.c_uint64, C.c_uint32, C.POINTER(C.c_void_p)]
     L.ta_plan_destroy.argtypes = [C.c_void_p]
@@ -139,7 +140,7 @@ def lib() -> C.CDLL:
 # Every symbol include/team_align_c.h declares (checked by tests/test_abi.py).
 ABI_SYMBOLS = [
     "ta_status_string", "ta_last_error", "ta_context_create", "ta_context_destroy", "ta_context_release",
-    "ta_context_held_bytes", "ta_set_default_device", "ta_current_device", "ta_device_count",
+    "ta_context_held_bytes", "ta_set_default_device", "ta_set_thread_device", "ta_current_device", "ta_device_count",
     "ta_cigar_slot_bytes", "ta_align_batch", "ta_align_batch_flags", "ta_plan_create", "ta_plan_destroy", "ta_plan_cigar_slots_bytes",
     "ta_plan_workspace_bytes", "ta_plan_chunks", "ta_plan_dual_pairs", "ta_plan_flex_pairs", "ta_plan_fused", "ta_plan_walk",
     "ta_plan_execute", "ta_plan_check", "ta_plan_execute_fill", "ta_plan_pair_chunks", "ta_affine_plan_pair_chunks", "ta_plan_execute_traceback", "ta_compact_cigars",

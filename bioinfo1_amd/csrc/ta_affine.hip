@@ -1329,7 +1329,7 @@ struct AffineHostPlan final : ta_host::HostPlan {
     uint64_t err_offset() const override {
         return pl->h.duals.empty() && pl->h.single_tasks.empty() ? UINT64_MAX : o.err;
     }
-    const char* err_message() const override {
+    const char* err_message(uint32_t) const override {
         return "affine fill: a pass hand-off poll timed out; results of this batch are invalid";
     }
 };

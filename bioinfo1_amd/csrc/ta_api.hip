@@ -164,7 +164,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
     if (h.ws_bnd_words)
         if (int r = ta_host::grow(ctx, ctx->ws_bnd, h.ws_bnd_words * 4ull)) return r;
     if (h.walk_group == 64 && h.want_cigar)
-        if (int r = ta_host::grow(ctx, ctx->ws_runs, 2 * h.slots_bytes + 64)) return r;
+        if (int r = ta_host::grow(ctx, ctx->ws_runs, 4 * (h.slots_bytes + 4))) return r;  // band_runs_off
     uint32_t* d_ptrs = static_cast<uint32_t*>(ctx->ws_ptrs.p);
     int32_t* d_bnd = static_cast<int32_t*>(ctx->ws_bnd.p);
     if (fill) {
@@ -319,6 +319,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
             // fill handed back ('-' bytes) in the one-pair walk: its list and count
             t.pflag = pl->d_pflag;
             t.runs = static_cast<uint32_t*>(ctx->ws_runs.p);
+            t.err = pl->d_err;
             t.fb_order = pl->d_fb + 2ull * ch.cbegin;
             t.fb_count = pl->d_fb + h.n_dual_pairs + c;
             TA_HIP(ctx, ta::launch_traceback(h.type, t, s, 64));
@@ -352,6 +353,11 @@ int exec(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t chunk, boo
 }
 
 // The linear plan as the host-memory batch driver sees it (ta_host_batch.h).
+const char* plan_err_message(uint32_t err) {
+    if (err & ta::kErrWalkCap) return "traceback: a band walk reached its event cap with cost left; results of this plan are invalid";
+    return "packed fill: a pass hand-off poll timed out; results of this plan are invalid";
+}
+
 struct LinearHostPlan final : ta_host::HostPlan {
     ta_plan* pl;
     PlanOffs o{};
@@ -365,9 +371,7 @@ struct LinearHostPlan final : ta_host::HostPlan {
     uint64_t err_offset() const override {
         return pl->h.flexes.empty() && pl->h.duals.empty() && pl->h.single_tasks.empty() ? UINT64_MAX : o.err;
     }
-    const char* err_message() const override {
-        return "packed fill: a pass hand-off poll timed out; results of this batch are invalid";
-    }
+    const char* err_message(uint32_t err) const override { return plan_err_message(err); }
 };
 
 }  // namespace
@@ -437,9 +441,10 @@ int ta_device_count(void) {
 uint64_t ta_context_held_bytes(const ta_context* ctx) {
     if (!ctx) return 0;
     uint64_t n = 0;
-    // only what a plan's workspace can reuse: the code and pass-boundary buffers
-    // (staging and output buffers are not handed to a plan's chunks)
-    for (const auto* b : {&ctx->ws_ptrs, &ctx->ws_bnd, &ctx->ws_runs}) n += b->cap;
+    // only what a plan's code workspace can reuse: the code and pass-boundary
+    // buffers (staging and output buffers are not handed to a plan's chunks, and
+    // the band walk's event words, ws_runs, are needed beside the codes)
+    for (const auto* b : {&ctx->ws_ptrs, &ctx->ws_bnd}) n += b->cap;
     return n;
 }
 
@@ -541,7 +546,7 @@ int ta_plan_check(ta_plan* pl) {
     TA_HIP(pl->ctx, hipMemcpy(&err, pl->d_err, 4, hipMemcpyDeviceToHost));
     if (!err) return TA_OK;
     TA_HIP(pl->ctx, hipMemset(pl->d_err, 0, 4));
-    return fail(pl->ctx, TA_ERR_DEVICE, "fill: a pass hand-off poll timed out; results of this plan are invalid");
+    return fail(pl->ctx, TA_ERR_DEVICE, plan_err_message(err));
 }
 
 int ta_compact_cigars(ta_context* ctx, uint32_t n_pairs, const char* cigar_slots, const uint64_t* cigar_start,

@@ -41,6 +41,10 @@ struct DualOut {
 constexpr int kDualStage = TA_DUAL_STAGE;
 static_assert(kDualStage == 0 || kDualStage == 8 || kDualStage == 16, "dual BLK staging");
 constexpr int kDualStageL = kDualStage ? kDualStage : 16;  // (array sizes and masks when staged)
+// the local gains as 32-bit adds in the M3 frame (dual_pass SW); 0: v_pk_add_u16
+#ifndef TA_SWAR
+#define TA_SWAR 1
+#endif
 
 struct DualIo {
     const uint8_t* Q[2];
@@ -110,6 +114,12 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // -gap*i term of S), so the left one carries gap twice
     const uint32_t GL = rep16(LOCAL ? 16 * gap + zstep : 2 * gap - ma);
     const uint32_t GUG = rep16(LOCAL ? 16 * gap - 1 : 0);  // up gain (no '-' in these queries)
+    // SW (with M3): the two gains as ONE 32-bit add each (ta_packed.h swar_add):
+    // every value and candidate of the M3 frame lies in [0, 0x7BFF]
+    // (local_max3_offset), so the low half never borrows from the high one
+    constexpr bool SW = M3 && TA_SWAR;
+    uint32_t GLk = swar_k(LOCAL ? 16 * gap + zstep : 2 * gap - ma), GUGk = swar_k(16 * gap - 1);
+    asm volatile("" : "+s"(GLk), "+s"(GUGk));  // SGPR operands (a literal would double the encoding)
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16 (see pk_min_u16)
     const uint32_t Tmax = pass_steps(m);
@@ -254,9 +264,9 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 constexpr int r = decltype(rc)::value;
                 const uint32_t old = H2[r];
                 const uint32_t diag = dnext;
-                const uint32_t left = pk_add(old, GL);
+                const uint32_t left = SW ? swar_add(old, GLk) : pk_add(old, GL);
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
-                const uint32_t up = LOCAL ? pk_add(upv, GUG) : upv;
+                const uint32_t up = LOCAL ? (SW ? swar_add(upv, GUGk) : pk_add(upv, GUG)) : upv;
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv;
                 if constexpr (M3) hv = pk_max3_pos_bc<r & 1>(m1, up, W[r / 2]);  // clamp folded in, :185

@@ -44,6 +44,11 @@ namespace {
 
 #ifdef TA_FLEX_MODE
 
+// the gains as 32-bit adds on the non-negative values (flex_pass SW); 0: v_pk_add_u16
+#ifndef TA_SWAR
+#define TA_SWAR 1
+#endif
+
 __device__ __forceinline__ int sext_lo(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 __device__ __forceinline__ int sext_hi(uint32_t x) { return (int)(int16_t)(x >> 16); }
 
@@ -127,8 +132,16 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     // folds into a three-input max (pk_max3_pos): the offsets start the
     // smallest clamp base of the wave at C0 and every rebase puts it back there
     // -- a margin for 64 steps of drift and one step of candidates below it.
+    // global / semi: every rebase puts lane 0's (or the last lane's) first row
+    // at C0 = 0x4000, the middle of the non-negative int16 range, which the
+    // wave's values leave by at most 15,000 (flex_fits).  So in every mode the
+    // values and candidates are non-negative int16 and the gains can be added
+    // by one 32-bit add per row (SW, ta_packed.h swar_add).
     const int amag = max(max(abs(ma), abs(mi)), abs(gap));
-    const int C0 = LOCAL ? 64 * abs(ma) + 16 * amag + 64 : 0;
+    const int C0 = LOCAL ? 64 * abs(ma) + 16 * amag + 64 : 0x4000;
+    constexpr bool SW = TA_SWAR != 0;
+    uint32_t GUGk = swar_k(gap - rowb);
+    asm volatile("" : "+s"(GUGk));
     // offsets: S(i, 0) = i * init, so start from the pass's first row
     int O[2] = {wmul(row_base, init - rowb) - C0, wmul(row_base, init - rowb) - C0};
     uint32_t q2[R], H2[R];
@@ -183,8 +196,8 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         // rebase (every 64 steps, all lanes alike): a lane that holds current cells;
         // local: the wave's smallest clamp base (lane 0 when ma >= 0: Z falls with
         // j) back to C0
-        const uint32_t d = LOCAL ? pk_sub((uint32_t)rdlane((int)Z, ma >= 0 ? 0u : 63u), rep16(C0))
-                                 : (uint32_t)rdlane((int)H2[0], t < M ? 0u : nl - 1);
+        const uint32_t d = pk_sub((uint32_t)rdlane(LOCAL ? (int)Z : (int)H2[0], LOCAL ? (ma >= 0 ? 0u : 63u) : (t < M ? 0u : nl - 1)),
+                                  rep16(C0));
 #pragma unroll
         for (int r = 0; r < R; ++r) H2[r] = pk_sub(H2[r], d);
         recv = pk_sub(recv, d);
@@ -246,11 +259,12 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)M));
         uint32_t acc0 = 0, acc1 = 0;
         if (active) {
-            uint32_t GL = rep16(glg);
+            uint32_t GL = rep16(glg), GLk = swar_k(glg);
             if (tdash) {
                 const int ga = ((tc2 & 0xFFFFu) == '-') ? gld : glg;
                 const int gb = ((tc2 >> 16) == '-') ? gld : glg;
                 GL = ((uint32_t)ga & 0xFFFFu) | ((uint32_t)gb << 16);
+                GLk = (uint32_t)(ga + gb * 65536);  // (per half: swar_add's constant)
             }
             auto e_of = [&](int r) {  // 0 on a match, 1 otherwise
                 if constexpr (CLS) return mismatch_flags(tA, tB, q2[r]);
@@ -262,9 +276,9 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 constexpr int r = decltype(rc)::value;
                 const uint32_t old = H2[r];
                 const uint32_t diag = dnext;
-                const uint32_t left = pk_add(old, GL);
+                const uint32_t left = SW ? swar_add(old, GLk) : pk_add(old, GL);
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
-                const uint32_t up = LOC ? pk_add(upv, GUG) : upv;
+                const uint32_t up = LOC ? (SW ? swar_add(upv, GUGk) : pk_add(upv, GUG)) : upv;
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv;
                 if constexpr (LOCAL) hv = pk_max3_pos(m1, up, Z);  // clamp folded in, :185

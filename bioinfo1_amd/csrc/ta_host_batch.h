@@ -35,7 +35,7 @@ struct HostPlan {
     virtual int execute(const ta_device_io* io, hipStream_t s) = 0;
     virtual uint64_t slots_bytes() const = 0;
     virtual uint64_t err_offset() const = 0;  // offset of the kernels' error word in the block, or UINT64_MAX
-    virtual const char* err_message() const = 0;
+    virtual const char* err_message(uint32_t err) const = 0;  // the error word's meaning
 };
 
 constexpr uint64_t kPackSeqLimit = 4ull << 20;  // sequences up to this travel inside the pinned block
@@ -46,8 +46,7 @@ constexpr uint64_t kSmallSlots = 4ull << 20;    // CIGAR slots up to this come b
 inline uint64_t batch_budget(const ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen,
                              int want_cigar, uint64_t bytes_per_entry) {
     if (!want_cigar) return 1ull << 30;
-    uint64_t need = 0;
-    for (uint32_t p = 0; p < n_pairs; ++p) need += ta::ptr_dwords(qlen[p], tlen[p]) * bytes_per_entry;
+    const uint64_t need = ta::host_batch_code_bytes(n_pairs, qlen, tlen, bytes_per_entry);
     return need <= (1ull << 30) ? std::max<uint64_t>(need, 1) : default_budget(ctx);
 }
 
@@ -161,7 +160,7 @@ inline int host_batch(ta_context* ctx, HostPlan& hp, uint32_t n_pairs, const cha
     if (err_off != UINT64_MAX) {
         uint32_t err = 0;
         std::memcpy(&err, hout + down, 4);
-        if (err) return fail(ctx, TA_ERR_DEVICE, hp.err_message());
+        if (err) return fail(ctx, TA_ERR_DEVICE, hp.err_message(err));
     }
     if (want_cigar) {
         const uint32_t* cl = reinterpret_cast<const uint32_t*>(hout + o_cl);

@@ -72,6 +72,16 @@ struct FillArgs {
     uint8_t* pflag;
 };
 
+// Bits of a plan's device error word (ta_plan_check, the host batches' status).
+constexpr uint32_t kErrPassPoll = 1u;  // a packed fill's pass hand-off poll gave up
+constexpr uint32_t kErrWalkCap = 2u;   // a band walk reached its event cap with cost left
+// First event word of pair p in a band walk's workspace: its CIGAR slot's byte
+// offset read as a word offset, rounded up to 4 words (16-byte stores).  Pair
+// p's room is then 2 (n + m) + 2 words - the rounding >= n + m + 1 events for
+// n + m >= 2 (the walk lists none for an empty pair); the workspace holds
+// slots_bytes + 4 words.
+__host__ __device__ inline uint64_t band_runs_off(uint64_t slot_off) { return (slot_off + 3u) & ~(uint64_t)3u; }
+
 struct TraceArgs {
     const uint32_t* order;
     uint32_t begin, count;
@@ -94,7 +104,8 @@ struct TraceArgs {
     int match, mismatch, gap;
     uint32_t blk;                // codes in the blocked layout (ta_layout.h blk_index)
     const uint8_t* pflag;        // band walk: pairs to leave to the fallback walk (FillArgs.pflag)
-    uint32_t* runs;              // band walks: run words, pair p's at runs + slot_off[p] / 2 (format_runs_kernel)
+    uint32_t* runs;              // band walks: event words, pair p's at runs + band_runs_off(slot_off[p]) (format_runs_kernel)
+    uint32_t* err;               // the plan's error word: band walks set kErrWalkCap
     const uint32_t* fb_order;    // band walks: the dual fill's hand-back list ('-' couples), walked after the band
     const uint32_t* fb_count;    // ... and its length (on the device)
 };

@@ -110,13 +110,35 @@ constexpr uint32_t kSignBytes = 0x0B0A0908u;
 __device__ __forceinline__ uint32_t sign_bytes(uint32_t dword_d, uint32_t dword_i) {
     return __builtin_amdgcn_perm(dword_d, dword_i, kSignBytes);
 }
-// v_bfi_b32 spelled out: from the C++ form hipcc builds and/or trees over
-// all 8 rows of a group, which keeps their sign bytes live (spills at 5 waves)
+// Bit select (a & mask) | (b & ~mask).  TA_BITOP3 (default): v_bitop3_b32
+// (gfx950, truth table 0xCA), which issues at ~2.5 cycles per wave64
+// instruction where v_bfi_b32 takes ~4.2 (profiles/r03_valu_rates.txt).  Not
+// the C++ form: from that hipcc builds and/or trees over all 8 rows of a group,
+// which keeps their sign bytes live (spills at 5 waves).
+#ifndef TA_BITOP3
+#define TA_BITOP3 1
+#endif
 __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
     uint32_t r;
+    // (inline asm, not __builtin_amdgcn_bitop3_b32: hipcc merges the builtin's
+    // chains into trees like the C++ form's, 15,988 spilled VGPRs in the dual fill)
+#if TA_BITOP3
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+#else
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(mask), "v"(a), "v"(b));
+#endif
     return r;
 }
+// Packed add of a per-half constant v through ONE 32-bit add (v_add_u32:
+// ~2.9 cycles per wave64 instruction against ~4.4 for v_pk_add_u16), exact
+// when every half of a and of the result lies in [0, 0x10000): then the low
+// half never borrows from or carries into the high one.  k = swar_k(v) =
+// v * 65537 (the low half's wrap-around carry pre-subtracted from the high
+// half when v < 0).  Used where values are range-proved non-negative int16
+// (ta_layout.h local_max3_offset).
+__device__ __forceinline__ uint32_t swar_k(int v) { return (uint32_t)(v * 65537); }
+__device__ __forceinline__ uint32_t swar_add(uint32_t a, uint32_t k) { return a + k; }
+
 // 0xFFFF in each half whose sign bit (15 / 31) is set
 __device__ __forceinline__ uint32_t half_mask(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x09090808u); }
 __device__ __forceinline__ uint32_t rep16(int v) { return ((uint32_t)v & 0xFFFFu) | ((uint32_t)v << 16); }

@@ -542,4 +542,10 @@ void build_affine_plan(AffinePlan& pl, uint32_t n_pairs, const uint32_t* qlen, c
     }
 }
 
+uint64_t host_batch_code_bytes(uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, uint64_t bytes_per_entry) {
+    uint64_t need = 0;
+    for (uint32_t p = 0; p < n_pairs; ++p) need += ptr_dwords_blk(qlen[p], tlen[p]) * bytes_per_entry;
+    return need;
+}
+
 }  // namespace ta

@@ -85,6 +85,13 @@ struct Plan {
 void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, int type, int match,
                 int mismatch, int gap, bool want_cigar, uint64_t budget, uint32_t flags, uint32_t wave_quantum = 0);
 
+// Code bytes a host batch (ta_align_batch: one chunk while they are <= 1 GiB)
+// reserves: per pair the blocked layout's size, which bounds the
+// [step][lane] layout's too -- the planner picks the layout after the budget
+// is set, and a budget of the smaller size split small batches of 1 kb local
+// pairs into two chunks (two launch sets, twice the drop-in latency, r04).
+uint64_t host_batch_code_bytes(uint32_t n_pairs, const uint32_t* qlen, const uint32_t* tlen, uint64_t bytes_per_entry);
+
 // Affine-gap plan (the extension of include/team_align_c.h).
 struct AffinePlan {
     uint32_t n_pairs = 0;

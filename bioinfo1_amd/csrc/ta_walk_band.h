@@ -222,7 +222,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
         P += a.ptr_off[p];
         Q += a.qoff[p];
         T += a.toff[p];
-        rout += a.slot_off[p] >> 1;  // 4 (n + m) bytes <= 2 x the slot
+        rout += band_runs_off(a.slot_off[p]);  // (16-byte aligned: bw_runs_out)
     }
     const uint32_t nb = blk_count(m);
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
@@ -385,6 +385,10 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
     atomicAdd(&bw_prof[6], (unsigned long long)bwp[6]);
     atomicAdd(&bw_prof[7], (unsigned long long)bwp[7]);
 #endif
+    // a walk stopped by the event cap with cost left would hand over a truncated
+    // CIGAR: the plan's error word says so (never on a correct walk: the cap is
+    // its columns plus stripe crossings)
+    if (has && H > 0) atomicOr(a.err, kErrWalkCap);
     if (has) {
         // the rest of the list (fewer than 40 events, in list order)
         for (uint32_t j = nout; j < nr; ++j) rout[j] = lds_ld32(rl + ((j & 63u) << 2));
@@ -448,7 +452,7 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
     if (a.pflag && a.pflag[p]) return;  // walked by the fallback walk
     const uint32_t n = a.qlen[p], m = a.tlen[p];
     const uint64_t cap = cigar_slot_bytes(n, m), soff = a.slot_off[p];
-    const uint32_t* ev = a.runs + (soff >> 1);
+    const uint32_t* ev = a.runs + band_runs_off(soff);
     char* end = a.slots + soff + cap;
     const uint32_t E = a.cigar_len[p];
 #ifdef TA_BW_DUMP

@@ -84,13 +84,18 @@ int env_device() {
     return d;
 }
 
+// This thread's device: set by ta_set_thread_device, else its current HIP
+// device read at its first call (or first call after ta_set_thread_device(-1)):
+// hipGetDevice costs ~6 µs per call on this runtime, a third of a small pair's
+// whole call.  -1: not read yet.
+thread_local int t_dev = -1;
+thread_local bool t_dev_pinned = false;  // set by ta_set_thread_device (outranks the process-wide choices)
+
 int call_device() {
+    if (t_dev_pinned) return t_dev;
     int d = g_default_device.load(std::memory_order_relaxed);
     if (d >= 0) return d;
     if ((d = env_device()) >= 0) return d;
-    // the thread's current device, read at its first call: hipGetDevice costs
-    // ~6 µs per call on this runtime, a third of a small pair's whole call
-    thread_local int t_dev = -1;
     if (t_dev < 0) t_dev = ta_current_device();
     return t_dev;
 }
@@ -342,5 +347,12 @@ int Align(const char* query, unsigned int query_len, const char* target, unsigne
 extern "C" int ta_set_default_device(int device) {
     if (device >= ta_device_count()) return TA_ERR_ARG;
     g_default_device.store(device < 0 ? -1 : device, std::memory_order_relaxed);
+    return TA_OK;
+}
+
+extern "C" int ta_set_thread_device(int device) {
+    if (device >= ta_device_count()) return TA_ERR_ARG;
+    t_dev = device < 0 ? -1 : device;  // -1: re-read the current HIP device at the next call
+    t_dev_pinned = device >= 0;
     return TA_OK;
 }

@@ -7,9 +7,9 @@
 set -euo pipefail
 ROOT="$(cd "$(dirname "$0")" && pwd)"
 CS="$ROOT/bioinfo1_amd/csrc"
-OUT="$ROOT/bioinfo1_amd/libteam_alignment.so"
+OUT="${TA_OUT:-$ROOT/bioinfo1_amd/libteam_alignment.so}"  # (experiment variants: TA_OUT, TA_BUILD_DIR, TA_LIB_ONLY=1)
 HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
-B="$ROOT/build"
+B="${TA_BUILD_DIR:-$ROOT/build}"
 mkdir -p "$B"
 FLAGS=(-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-result -Wno-unused-function ${TA_EXTRA_FLAGS:-})
 pids=()
@@ -51,6 +51,7 @@ cc "$B/shim.o" "$CS/team_alignment_shim.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$
 # host planner: plain C++ (also built with g++ under ASan/UBSan/TSan by tests/test_host_sanitizers.py)
 cc "$B/ta_planner.o" "$CS/ta_planner.cpp" g++ -O2 -std=c++17 -fPIC -Wall -c "$CS/ta_planner.cpp"
 # mapper stages (libteam_mapper.so) and the team_mapper_amd CLI
+if [ "${TA_LIB_ONLY:-0}" != 1 ]; then
 for f in tm_minimizers tm_match tm_chain; do
   cc "$B/$f.o" "$CS/$f.hip" "$HIPCC" "${FLAGS[@]}" -c "$CS/$f.hip"
 done
@@ -58,9 +59,11 @@ for f in tm_api tm_fastx; do
   cc "$B/$f.o" "$CS/$f.cpp" "$HIPCC" "${FLAGS[@]}" -x hip -c "$CS/$f.cpp"
 done
 cc "$B/tm_main.o" "$CS/tm_main.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp"
+fi
 for p in "${pids[@]}"; do wait "$p"; done
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_dual_blk.o" "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_server.o" "$B/ta_planner.o" "$B/shim.o" \
   -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$OUT"
+if [ "${TA_LIB_ONLY:-0}" = 1 ]; then echo "built $OUT"; exit 0; fi
 PKG="$ROOT/bioinfo1_amd"
 "$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/tm_{minimizers,match,chain,api,fastx}.o -L"$PKG" -lteam_alignment -lz \
   -Wl,-rpath,'$ORIGIN' -o "$PKG/libteam_mapper.so"

@@ -108,6 +108,12 @@ int ta_server_last_times(const ta_server* server, uint32_t slot, double* us_out4
  * call (a thread keeps it: hipGetDevice per call would cost more than a small
  * pair's alignment).  TA_ERR_ARG for a device that does not exist. */
 int ta_set_default_device(int device);
+/* The calling thread's own choice, ahead of the three above: its drop-in calls
+ * run on `device` (>= 0).  -1 drops the choice and makes the thread's next
+ * call read its current HIP device again -- the call to make after a
+ * hipSetDevice that should move the thread's team::Align calls with it.
+ * TA_ERR_ARG for a device that does not exist. */
+int ta_set_thread_device(int device);
 /* The calling thread's current HIP device (0 when it has none) and the number of devices. */
 int ta_current_device(void);
 int ta_device_count(void);

@@ -1,6 +1,9 @@
 """Experiment: host-to-host latency of small ta_align_batch_flags batches
-(200x200 and 1000x1000 local pairs), int32-fused plan vs the default plan."""
+(200x200 and 1000x1000 local pairs) under plan flags (BL_FLAGS, default
+"1,0": the int32-fused plan vs the default plan; "0,128": the default plan vs
+TA_PLAN_NO_BLK, the [step][lane] layout and lane walks)."""
 import ctypes as C
+import os
 import sys
 import time
 
@@ -18,13 +21,13 @@ def p(a, t):
     return a.ctypes.data_as(C.POINTER(t))
 
 
-for shape in (200, 1000):
-    for n in (1, 2, 4, 8, 16, 64):
+for shape in [int(x) for x in os.environ.get("BL_SHAPES", "200,1000").split(",")]:
+    for n in [int(x) for x in os.environ.get("BL_N", "1,2,4,8,16,64").split(",")]:
         b = synth.uniform_batch(n, shape, shape)
         cap = int((2 * (b.qlen.astype(np.uint64) + b.tlen.astype(np.uint64)) + 2).sum())
         arena = np.zeros(cap, np.uint8)
         sc = np.zeros(n, np.int32); tb = np.zeros(n, np.uint32); coff = np.zeros(n, np.uint64); clen = np.zeros(n, np.uint32)
-        for flags in (1, 0):
+        for flags in [int(x) for x in os.environ.get("BL_FLAGS", "1,0").split(",")]:
             ts = []
             for it in range(30):
                 t0 = time.perf_counter()

@@ -5,8 +5,12 @@
 
 Writes profiles/<round-tag>_kernel_stats.csv (the rocprofv3 --stats summary),
 profiles/<round-tag>_pmc.json (per-kernel average counters per dispatch) and
-merges per-launch HBM traffic of the fill kernel into profiles/traffic.json
-and VALU instructions per DP cell into profiles/valu.json (read by bench.py).
+merges the dominant fill kernel's HBM traffic per step and its VALU
+instructions per DP cell into profiles/traffic_by_kernel.json and
+profiles/valu_by_kernel.json, keyed "<kernel>|<workload-tag>" with the kernel
+named as rocprofv3 prints it (bench.py dominant_kernel reads the same key, so a
+line never quotes another kernel's counters).  profiles/traffic.json and
+valu.json are the r01-r04 tables keyed by workload alone (history).
 
 HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE and WRITE_SIZE come
 from separate passes; FETCH_SIZE is reported in KB and reads 1/2 of the bytes
@@ -50,6 +54,20 @@ def bench_line(d):
     return None
 
 
+def short_name(k):
+    """'void ta::(anonymous namespace)::dual_fill_kernel<1, true, true>(ta::FillArgs)'
+    -> 'dual_fill_kernel<1, true, true>' (bench.py dominant_kernel's form)"""
+    k = k.split("(ta::")[0] if "(ta::" in k else k
+    return k.replace("void ", "").replace("ta::(anonymous namespace)::", "").strip()
+
+
+def merge(path, key, entry):
+    d = json.load(open(path)) if os.path.exists(path) else {}
+    d[key] = entry
+    with open(path, "w") as fh:
+        json.dump(dict(sorted(d.items())), fh, indent=1)
+
+
 def main():
     src, rtag, wtag = sys.argv[1], sys.argv[2], sys.argv[3]
     prof = os.path.join(ROOT, "profiles")
@@ -75,18 +93,17 @@ def main():
         tr = None
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             tr = int((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024 * per_step)
-        p = os.path.join(prof, "traffic.json")
-        d = json.load(open(p)) if os.path.exists(p) else {}
-        d[wtag] = tr
-        json.dump(d, open(p, "w"), indent=1)
+        key = f"{short_name(k)}|{wtag}"
+        meta = {"profile": rtag, "kernel": k, "dispatches_per_step": per_step}
+        if bl and (bl.get("roofline") or {}).get("kernel") not in (None, short_name(k)):
+            print("WARNING: bench line names", bl["roofline"]["kernel"], "but the dominant PMC kernel is", k)
+        merge(os.path.join(prof, "traffic_by_kernel.json"), key, dict(value=tr, **meta))
         if "SQ_INSTS_VALU" in cs:
             # SQ_INSTS_VALU counts wave-instructions; cells per step from the bench line
             cells = bl["config"]["cells_per_gpu"]
             # per lane-cell: wave-instr x 64 lanes / cells
-            p = os.path.join(prof, "valu.json")
-            d = json.load(open(p)) if os.path.exists(p) else {}
-            d[wtag] = round(cs["SQ_INSTS_VALU"] * 64 * per_step / cells, 3)
-            json.dump(d, open(p, "w"), indent=1)
+            merge(os.path.join(prof, "valu_by_kernel.json"), key,
+                  dict(value=round(cs["SQ_INSTS_VALU"] * 64 * per_step / cells, 3), **meta))
         print(k, json.dumps(cs, indent=1))
     print("summary written to", prof)
 

@@ -28,13 +28,17 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 CS = os.path.join(ROOT, "bioinfo1_amd", "csrc")
 SIMDS, CLOCK = 256 * 4, 2.4e9
 
-# kernel tag -> (source, defines, kernel symbol substring)
+# kernel (as rocprofv3 names it; bench.py dominant_kernel) -> (source, defines, symbol substring)
 KERNELS = {
-    "dual_fill_kernel<kLocal,true>": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1"], "dual_fill_kernelILi1ELb1E"),
-    "dual_fill_kernel<kSemi,true>": ("ta_dual.hip", ["-DTA_DUAL_MODE=2", "-DTA_DUAL_CIGAR=1"], "dual_fill_kernelILi2ELb1E"),
-    "flex_fill_kernel<kSemi,true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=2", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi2ELb1E"),
-    "flex_fill_kernel<kLocal,true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=1", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi1ELb1E"),
-    "affine_dual_fill_kernel<kSemi,true>": ("ta_affine.hip", [], "affine_dual_fill_kernelILi2ELb1E"),
+    "dual_fill_kernel<1, true, true>": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1", "-DTA_DUAL_BLK"],
+                                        "dual_fill_kernelILi1ELb1ELb1E"),
+    "dual_fill_kernel<1, true, false>": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1"],
+                                         "dual_fill_kernelILi1ELb1ELb0E"),
+    "dual_fill_kernel<2, true, false>": ("ta_dual.hip", ["-DTA_DUAL_MODE=2", "-DTA_DUAL_CIGAR=1"],
+                                         "dual_fill_kernelILi2ELb1ELb0E"),
+    "flex_fill_kernel<2, true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=2", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi2ELb1E"),
+    "flex_fill_kernel<1, true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=1", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi1ELb1E"),
+    "affine_dual_fill_kernel<2, true>": ("ta_affine.hip", [], "affine_dual_fill_kernelILi2ELb1E"),
 }
 
 

@@ -141,7 +141,7 @@ void check_linear(const ta::Plan& pl, uint64_t budget) {
         if (c.ptr_dwords * 4 > budget) CHECK(c.scount + c.dcount + c.fcount == 1);
         for (uint32_t k = c.begin; k < c.begin + c.count; ++k) {
             const uint32_t x = pl.order[k];
-            const uint64_t need = pl.want_cigar ? ta::ptr_dwords(pl.qlen[x], pl.tlen[x]) : 0;
+            const uint64_t need = pl.want_cigar ? ta::ptr_dwords_any(pl.qlen[x], pl.tlen[x], pl.blk) : 0;
             CHECK(pl.ptr_off[x] + need <= c.ptr_dwords);
             CHECK(pl.bnd_off[x] + ta::bnd_words(pl.qlen[x], pl.tlen[x]) <= c.bnd_words);
         }
@@ -277,7 +277,29 @@ void plan_worker(uint64_t seed, int iters) {
     }
 }
 
+// Small host batches (the drop-in call's combined batches, ta_align_batch)
+// plan as ONE chunk under their own budget (ta_host_batch.h batch_budget), in
+// both code layouts.
+void check_small_batches() {
+    const uint32_t shapes[][2] = {{1000, 1000}, {200, 200}, {5, 9}, {1000, 700}, {3000, 2500}};
+    for (const auto& sh : shapes)
+        for (uint32_t P : {1u, 2u, 3u, 8u, 16u, 33u})
+            for (int type = 0; type < 3; ++type)
+                for (uint32_t flags : {0u, 128u}) {  // 128: TA_PLAN_NO_BLK
+                    std::vector<uint32_t> q(P, sh[0]), t(P, sh[1]);
+                    const uint64_t budget = std::max<uint64_t>(ta::host_batch_code_bytes(P, q.data(), t.data(), 4), 1);
+                    ta::Plan pl;
+                    ta::build_plan(pl, P, q.data(), t.data(), type, 1, -1, -1, true, budget, flags, 1024);
+                    check_linear(pl, budget);
+                    CHECK(pl.chunks.size() == 1);
+                    if (pl.chunks.size() != 1)
+                        std::printf("small batch %u x %ux%u type %d flags %u: %zu chunks\n", P, sh[0], sh[1], type, flags,
+                                    pl.chunks.size());
+                }
+}
+
 int run_planner(uint64_t seed, int iters, int threads) {
+    check_small_batches();
     std::vector<std::thread> th;
     for (int w = 0; w < threads; ++w) th.emplace_back(plan_worker, seed + (uint64_t)w * 7919, iters);
     for (auto& x : th) x.join();

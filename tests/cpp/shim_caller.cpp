@@ -7,6 +7,7 @@
 // the cases are run from argv[2] (default 4) threads at once (the mapper's
 // OpenMP loop).
 #include <cstdio>
+#include <cstring>
 #include <iostream>
 #include <sstream>
 #include <string>
@@ -54,7 +55,54 @@ static void run(Case& c) {
     }
 }
 
+// (weak: defined only by the CPU stand-in tests/cpp/stub_ta.cpp; the GPU tests
+// link this caller against the real library and never run "devices")
+extern "C" __attribute__((weak)) void stub_set_current_device(int);
+extern "C" __attribute__((weak)) int stub_last_device();
+extern "C" int ta_set_thread_device(int);
+
+// "devices": which device a thread's calls run on (include/team_align_c.h,
+// ta_set_thread_device): its current device as of its first call, kept across
+// a later device switch, re-read after ta_set_thread_device(-1), and a pinned
+// device ahead of the current one -- on the server path (even query lengths,
+// stub_ta.cpp) and on the batch path (odd ones).
+int run_devices() {
+    if (!stub_set_current_device || !stub_last_device) {
+        std::printf("devices: needs the CPU stand-in (stub_ta.cpp)\n");
+        return 2;
+    }
+    int bad = 0;
+    auto call = [&](const char* q, int want, const char* what) {
+        std::string cig;
+        unsigned tb = 0;
+        team::Align(q, (unsigned)std::strlen(q), "ACGTACGT", 8, team::AlignmentType::local, 1, -1, -1, &cig, &tb);
+        if (stub_last_device() != want) {
+            std::printf("%s: device %d, want %d\n", what, stub_last_device(), want);
+            ++bad;
+        }
+    };
+    for (const char* q : {"ACGT", "ACG"}) {  // server path, batch path
+        std::thread([&] {
+            stub_set_current_device(1);
+            call(q, 1, "first call");
+            stub_set_current_device(2);
+            call(q, 1, "after a device switch (kept)");
+            if (ta_set_thread_device(-1) != 0) ++bad;
+            call(q, 2, "after ta_set_thread_device(-1)");
+            if (ta_set_thread_device(3) != 0) ++bad;
+            stub_set_current_device(0);
+            call(q, 3, "pinned");
+            if (ta_set_thread_device(99) == 0) ++bad;  // no such device
+            call(q, 3, "pinned after a refused choice");
+        }).join();
+        std::thread([&] { call(q, 0, "another thread"); }).join();
+    }
+    std::printf("devices %s\n", bad ? "FAIL" : "ok");
+    return bad ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc > 1 && std::string(argv[1]) == "devices") return run_devices();
     std::vector<Case> cases;
     std::string line;
     while (std::getline(std::cin, line)) {

@@ -41,21 +41,27 @@ int ta_context_create(int device, ta_context** out) {
 
 void ta_context_destroy(ta_context* ctx) { delete ctx; }
 
-int ta_current_device(void) { return 0; }
-int ta_device_count(void) { return 1; }
+// the thread's "current device" (stub_set_current_device) and the device of
+// the last call served for this thread (stub_last_device): the device-choice
+// test of tests/cpp/shim_caller.cpp ("devices")
+thread_local int t_stub_current = 0, t_stub_last = -1;
+void stub_set_current_device(int d) { t_stub_current = d; }
+int stub_last_device() { return t_stub_last; }
+int ta_current_device(void) { return t_stub_current; }
+int ta_device_count(void) { return 4; }
 
 // The single-pair server: the oracle again, for pairs of even query length
 // (the others take the shim's batch path, so both run under TSan).
 struct ta_server {
-    int type = 0;
+    int type = 0, device = 0;
     std::atomic<int> active{0}, paused{0};  // the pause protocol of ta_server.cpp
 };
 
 int ta_server_create(int device, int type, uint32_t slots, ta_server** out) {
-    (void)device;
     (void)slots;
     *out = new ta_server();
     (*out)->type = type;
+    (*out)->device = device;
     return TA_OK;
 }
 
@@ -91,6 +97,7 @@ int ta_server_align(ta_server* s, const char* q, uint32_t n, const char* t, uint
         std::atomic<int>& a;
         ~Leave() { a.fetch_sub(1); }
     } leave{s->active};
+    t_stub_last = s->device;
     int sc = 0;
     unsigned b = 0;
     size_t cl = 0;
@@ -110,6 +117,7 @@ int ta_align_batch(ta_context* ctx, uint32_t n_pairs, const char* qb, const uint
                    int gap, int want_cigar, int32_t* score, uint32_t* target_begin, char* arena, uint64_t arena_bytes,
                    uint64_t* cigar_off, uint32_t* cigar_len) {
     uint64_t at = 0;
+    t_stub_last = ctx->device;  // (the leader's thread: the device-choice test runs one thread)
     for (uint32_t p = 0; p < n_pairs; ++p) {
         int s = 0;
         unsigned b = 0;

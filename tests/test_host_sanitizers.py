@@ -94,6 +94,17 @@ def test_planner_tsan():
     assert "fails 0" in _run([exe, "planner", "777", "40", "8"])
 
 
+def test_dropin_shim_thread_device():
+    """A thread's team::Align calls follow ta_set_thread_device / its first
+    call's device (include/team_align_c.h), on both shim paths."""
+    exe = _build("shim_tsan", "-fsanitize=thread",
+                 extra_c=[os.path.join(ROOT, "oracle", "align_oracle.c")],
+                 extra_cpp=[os.path.join(ROOT, "tests", "cpp", "shim_caller.cpp"),
+                            os.path.join(CS, "team_alignment_shim.cpp"), os.path.join(ROOT, "tests", "cpp", "stub_ta.cpp")])
+    r = subprocess.run([exe, "devices"], capture_output=True, text=True, env=ENV, timeout=300)
+    assert r.returncode == 0 and "ThreadSanitizer" not in r.stderr and "devices ok" in r.stdout, (r.stdout, r.stderr[-3000:])
+
+
 def test_dropin_shim_tsan(kat_cases, random_cases):
     """team::Align's shim from 4 threads (the mapper's OpenMP loop) under TSan."""
     exe = _build("shim_tsan", "-fsanitize=thread",
