@@ -234,6 +234,16 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     units.reserve(n_pairs);
     std::vector<uint32_t> rest;
     const bool flex_ok = dual && !(flags & kPlanNoFlex) && flex_fits(type, match, mismatch, gap);
+    // A pair left without a partner (an odd pair of equal shapes, a ragged pair no
+    // neighbour couples with) runs coupled with itself in the dual kernel, like a
+    // lone pair, rather than in the int32 fill: a drop-in batch of 3 x 1 kb went
+    // 1.12 -> 0.78 ms with the packed fill and walk for all of its pairs
+    // (profiles/bench/r05_batch_latency.txt).
+    // (tiny pairs keep the int32 fill: alone, its one fused launch is the shortest)
+    auto lone_dual = [&](uint32_t p) {
+        return dual && (uint64_t)qlen[p] * tlen[p] >= 4096 && n_passes(qlen[p]) < 64 &&
+               fits_int16(type, qlen[p], tlen[p], match, mismatch, gap);
+    };
     for (uint32_t k = 0; k < n_pairs;) {
         const uint32_t p = order[k];
         const uint32_t n = qlen[p], m = tlen[p];
@@ -289,13 +299,17 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
                     continue;
                 }
             }
-            // a long pair without a partner is coupled with itself: one wave per pass
+            // a long pair without a partner is coupled with itself: one wave per pass;
+            // a shorter one in the dual kernel when it fits int16 (lone_dual)
             const uint32_t ps = n_passes(qlen[A]);
-            units.push_back({ps >= 4 && ps < 64 ? 2 : 0, A, A, (uint64_t)qlen[A] * tlen[A]});
+            if (ps >= 4 && ps < 64)
+                units.push_back({2, A, A, (uint64_t)qlen[A] * tlen[A]});
+            else
+                units.push_back({lone_dual(A) ? 1 : 0, A, A, (uint64_t)qlen[A] * tlen[A]});
             ++i;
         }
     } else {
-        for (uint32_t p : rest) units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
+        for (uint32_t p : rest) units.push_back({lone_dual(p) ? 1 : 0, p, p, (uint64_t)qlen[p] * tlen[p]});
     }
     std::stable_sort(units.begin(), units.end(), [](const Unit& x, const Unit& y) { return x.cost > y.cost; });
     // Local walks of short pairs in plans of equal-shape couples only run as band
@@ -305,9 +319,12 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     uint64_t len_sum = 0;
     for (uint32_t p = 0; p < n_pairs; ++p) len_sum += (uint64_t)qlen[p] + tlen[p];
     const bool short_pairs = len_sum <= 6000ull * std::max<uint32_t>(n_pairs, 1);
+    // (batches of fewer than 8 pairs -- drop-in calls -- keep the lane walks: one band-walk
+    // lane per pair leaves a lone wave's dependent chain ~50 us longer for 1-2 pairs of
+    // 1 kb, scripts/exp/batch_latency.py, profiles/bench/r05_batch_latency.txt)
     bool all_dual = !units.empty();
     for (const Unit& u : units) all_dual = all_dual && u.kind == 1;
-    pl.blk = want_cigar && type == kLocal && all_dual && short_pairs && mag < (1ull << 22) &&
+    pl.blk = want_cigar && type == kLocal && all_dual && short_pairs && n_pairs >= 8 && mag < (1ull << 22) &&
              !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2));
     // Multi-pass int32 pairs run one wave per (pair, pass) like the packed
     // fills (their passes overlap instead of following each other on one

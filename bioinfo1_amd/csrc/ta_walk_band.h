@@ -473,10 +473,14 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
         used = 2;
     }
     uint32_t cop = 3u, ccnt = 0u;  // the run carried from the previous round (op 3: none)
+    // each round's events are loaded one round ahead: the text stores of a round
+    // (char, which may alias anything) keep the compiler from hoisting the load
+    uint32_t vnext = (uint32_t)lane < E ? ev[lane] : 0u;
     for (uint32_t base = 0; base < E; base += 64u) {
         const uint32_t k = base + (uint32_t)lane;
         const bool act = k < E;
-        const uint32_t v = act ? ev[k] : 0u;
+        const uint32_t v = vnext;
+        vnext = k + 64u < E ? ev[k + 64u] : 0u;
         const uint32_t kd = v >> 2, mop = act ? (v & 3u) : 3u;
         const bool va = kd > 0, vb = mop != 3u;      // item A: D x kd; item B: the move (M / I) x 1
         const uint32_t first = va ? 2u : mop;        // op of the event's first / last item (3: no item)
