@@ -25,9 +25,13 @@
 //    are stored only for its own steps, its column-m candidates and corner
 //    are captured when the lanes reach column mB, its row-n best only counts
 //    columns <= mB and is read from its own last lane.
-//  * Local mode (team_alignment.cpp:171-194).  The same V; the clamp H >= 0
-//    is V >= Z with Z = -ma*j - O, one packed value per lane and step (all 16
-//    rows share j).  The reference's argmax is the first strict maximum in
+//  * Local mode (team_alignment.cpp:171-194).  S = H - ma*j + gap*(j - i) as
+//    in global / semi (the up candidate is the value above itself), held in
+//    the lane frame V + (17*gap - ma)*lane (ta_layout.h flex_local_c0), in
+//    which the clamp H >= 0 of row r of every lane is V >= zu - gap*r with zu
+//    uniform over the wave: the 16 bases of a step are 8 SGPRs (two rows per
+//    register, picked by op_sel, as ta_dual.hip) and a rebase is one scalar.
+//    The reference's argmax is the first strict maximum in
 //    row-major order.  Per step each lane ranks its 16 rows by the key
 //    16*(V_r - V_0) + 15 - r (rows of one column differ by at most
 //    |score| + |gap| each, so it fits int16: larger H first, then the smaller
@@ -111,12 +115,10 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     constexpr int R = kRows;
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const int init = (MODE == kGlobal) ? gap : 0;
-    constexpr bool LOC = MODE == kLocal;
-    const int rowb = LOC ? 0 : gap;  // global / semi: the -gap*i term of S (none in local)
+    const int rowb = gap;  // the -gap*i term of S (the up gain is 0)
     const uint32_t KD = rep16(mi - ma);
     const int glg = gap - ma + rowb;  // left gain, target byte != '-'
     const int gld = -ma + rowb;       // left gain, target byte == '-'
-    const uint32_t GUG = rep16(gap - rowb);  // up gain (0 in global / semi)
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16
     const uint32_t M = max(io.m[0], io.m[1]);
@@ -129,19 +131,21 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
 
     constexpr bool LOCAL = MODE == kLocal;
     // local: every value is kept in [0, 0x7BFF] (flex_local_fits) so the clamp
-    // folds into a three-input max (pk_max3_pos): the offsets start the
-    // smallest clamp base of the wave at C0 and every rebase puts it back there
-    // -- a margin for 64 steps of drift and one step of candidates below it.
+    // folds into a three-input max (pk_max3_pos_bc): every rebase puts the
+    // wave-uniform row-0 clamp base zu at C0 (ta_layout.h flex_local_c0) -- a
+    // margin for 64 steps of drift and one step of candidates below it.
     // global / semi: every rebase puts lane 0's (or the last lane's) first row
     // at C0 = 0x4000, the middle of the non-negative int16 range, which the
     // wave's values leave by at most 15,000 (flex_fits).  So in every mode the
     // values and candidates are non-negative int16 and the gains can be added
     // by one 32-bit add per row (SW, ta_packed.h swar_add).
-    const int amag = max(max(abs(ma), abs(mi)), abs(gap));
-    const int C0 = LOCAL ? 64 * abs(ma) + 16 * amag + 64 : 0x4000;
+    const int C0 = LOCAL ? flex_local_c0(ma, mi, gap) : 0x4000;
     constexpr bool SW = TA_SWAR != 0;
-    uint32_t GUGk = swar_k(gap - rowb);
-    asm volatile("" : "+s"(GUGk));
+    // local: the lane frame (+ dl * lane; the hand-off adds dl) and the row-0 clamp
+    // base zu of the current step, the same in every lane (t = -1 here)
+    const int dl = LOCAL ? 17 * gap - ma : 0;
+    const uint32_t D2 = rep16(dl);
+    int zu = C0 - gap;
     // offsets: S(i, 0) = i * init, so start from the pass's first row
     int O[2] = {wmul(row_base, init - rowb) - C0, wmul(row_base, init - rowb) - C0};
     uint32_t q2[R], H2[R];
@@ -150,15 +154,11 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         const uint32_t i0 = row_base + (uint32_t)lane * R + r;
         const uint32_t qa = i0 < io.n[0] ? (uint32_t)io.Q[0][i0] : 0u, qb = i0 < io.n[1] ? (uint32_t)io.Q[1][i0] : 0u;
         q2[r] = CLS ? row_selector(qa, qb) : (qa | (qb << 16));
-        H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init - rowb) + C0);  // S(i, 0) - O
+        H2[r] = rep16(wmul((uint32_t)lane * R + r + 1, init - rowb) + C0 + dl * lane);  // S(i, 0) - O (+ frame)
     }
-    uint32_t recv = rep16(wmul((uint32_t)lane * R, init - rowb) + C0);
+    uint32_t recv = rep16(wmul((uint32_t)lane * R, init - rowb) + C0 + dl * lane);
     uint32_t tc2 = 0, tA = 0x01010101u, tB = 0x01010101u;
-    // local: clamp base Z = -ma*j - O per half (j = -lane before step 0), ma*j
-    // (int32), the running best key 16*H + 15 - r and its column per pair
-    const uint32_t MA2 = rep16(ma);
-    uint32_t Z = LOCAL ? rep16(ma * lane + C0) : 0u;
-    int mj = -ma * lane;
+    // local: the running best key 16*H + 15 - r and its column per pair
     int bestk[2] = {INT_MIN, INT_MIN};
     uint32_t bestj[2] = {0, 0};
     // captures (absolute int32): column m_h candidates (semi) / corner (global), row-n best (semi)
@@ -193,15 +193,13 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         if (pass > 0) {
             load_rec_chunk(io, M, t >> 6, lane, bcur);
         }
-        // rebase (every 64 steps, all lanes alike): a lane that holds current cells;
-        // local: the wave's smallest clamp base (lane 0 when ma >= 0: Z falls with
-        // j) back to C0
-        const uint32_t d = pk_sub((uint32_t)rdlane(LOCAL ? (int)Z : (int)H2[0], LOCAL ? (ma >= 0 ? 0u : 63u) : (t < M ? 0u : nl - 1)),
-                                  rep16(C0));
+        // rebase (every 64 steps, all lanes alike): a lane that holds current cells
+        // to C0; local: the row-0 clamp base zu back to C0 (both pairs alike)
+        const uint32_t d = LOCAL ? rep16(zu - C0) : pk_sub((uint32_t)rdlane((int)H2[0], t < M ? 0u : nl - 1), rep16(C0));
 #pragma unroll
         for (int r = 0; r < R; ++r) H2[r] = pk_sub(H2[r], d);
         recv = pk_sub(recv, d);
-        if (LOCAL) Z = pk_sub(Z, d);
+        if (LOCAL) zu = C0;
         O[0] += sext_lo(d);
         O[1] += sext_hi(d);
     };
@@ -231,10 +229,10 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         constexpr bool MASKED = decltype(masked_tag)::value;
         uint32_t top;
         if (pass == 0) {
-            const int s0 = (init - ma + rowb) * (int)(t + 1);  // S(0, j)
+            const int s0 = (init - ma + rowb) * (int)(t + 1) - dl;  // S(0, j) (local: - dl, added back by the hand-off)
             top = ((uint32_t)(s0 - O[0]) & 0xFFFFu) | ((uint32_t)(s0 - O[1]) << 16);
         } else {
-            const int ba = rdlane(bcur[0], t & 63u), bb = rdlane(bcur[1], t & 63u);
+            const int ba = rdlane(bcur[0], t & 63u) - dl, bb = rdlane(bcur[1], t & 63u) - dl;
             top = ((uint32_t)(ba - O[0]) & 0xFFFFu) | ((uint32_t)(bb - O[1]) << 16);
         }
         const uint32_t sh = (t & 3u) * 8;
@@ -243,6 +241,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
         const uint32_t prev = recv;
         recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
+        if constexpr (LOCAL) recv = pk_add(recv, D2);  // into this lane's frame
         if constexpr (CLS) {
             tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
             tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
@@ -250,10 +249,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         } else {
             tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
         }
-        if (LOCAL) {
-            Z = pk_sub(Z, MA2);
-            mj += ma;
-        }
+        if (LOCAL) zu += gap - ma;
 
         const int j = (int)t - lane + 1;
         const bool active = !MASKED || (((uint32_t)lane < nl) & (j >= 1) & (j <= (int)M));
@@ -272,16 +268,24 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             };
             uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
             uint32_t upv = recv;
+            // local: the clamp bases of rows 2k, 2k + 1 in the halves of W[k] (op_sel
+            // picks one for both pairs), wave-uniform (SALU); all >= 0, no borrows
+            uint32_t W[R / 2];
+            if constexpr (LOCAL) {
+                W[0] = ((uint32_t)zu & 0xFFFFu) | ((uint32_t)(zu - gap) << 16);
+#pragma unroll
+                for (int k = 1; k < R / 2; ++k) W[k] = W[0] - (uint32_t)(2 * k * gap) * 0x10001u;
+            }
             static_for<0, R>([&](auto rc) {
                 constexpr int r = decltype(rc)::value;
                 const uint32_t old = H2[r];
                 const uint32_t diag = dnext;
                 const uint32_t left = SW ? swar_add(old, GLk) : pk_add(old, GL);
                 if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
-                const uint32_t up = LOC ? (SW ? swar_add(upv, GUGk) : pk_add(upv, GUG)) : upv;
+                const uint32_t up = upv;  // the value above itself (S's -gap*i term)
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv;
-                if constexpr (LOCAL) hv = pk_max3_pos(m1, up, Z);  // clamp folded in, :185
+                if constexpr (LOCAL) hv = pk_max3_pos_bc<r & 1>(m1, up, W[r / 2]);  // clamp folded in, :185
                 else hv = pk_max(m1, up);
                 if (CIGAR) {
                     // raw compares (D wins over I in the walk; local walks track the cost)
@@ -295,13 +299,15 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             });
             if (LOCAL) {
                 // the lane's best row of this column per pair: key 16*(V_r - V_0) + 15 - r,
-                // + kKeyOff so that the keys are non-negative for the three-input max tree
-                constexpr int kKeyOff = 4096;  // |16*(V_r - V_0)| <= 16*15*2*mag < 4096 (flex_fits)
+                // + kKeyOff so that the keys are non-negative for the three-input max tree.
+                // H_r - H_0 = V_r - V_0 + gap*r (row r's clamp base is gap*r below row 0's);
+                // |16*(H_r - H_0)| <= 16*15*2*mag < 4096 (flex_fits)
+                constexpr int kKeyOff = 4096;
                 uint32_t K[R];
                 K[0] = rep16(kKeyOff + 15);
 #pragma unroll
                 for (int r = 1; r < R; ++r)
-                    K[r] = pk_mad_i16(pk_sub(H2[r], H2[0]), 0x00100010u, rep16(kKeyOff + 15 - r));
+                    K[r] = pk_mad_i16(pk_sub(H2[r], H2[0]), 0x00100010u, rep16(kKeyOff + 15 - r + 16 * gap * r));
                 const uint32_t lo = max3_reduce<NV>(K);
                 uint32_t kA = lo, kB = lo;
                 if constexpr (NV != R) {  // the pair's last lane holds NV valid rows
@@ -313,8 +319,9 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 const int v0[2] = {sext_lo(H2[0]), sext_hi(H2[0])};
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
-                    // 16*H + 15 - r = 16*(V_0 + O + ma*j) + key (cells of this pair only)
-                    const int key = ((v0[h] + O[h] + mj) << 4) + kk[h];
+                    // 16*H + 15 - r = 16*H_0 + key (cells of this pair only), where H_0 = V_0 - zu:
+                    // row 0's value above its clamp base (the lane frame and O cancel)
+                    const int key = ((v0[h] - zu) << 4) + kk[h];
                     const bool better = (uint32_t)lane < nlh[h] && j <= (int)io.m[h] && key > bestk[h];
                     bestk[h] = better ? key : bestk[h];
                     bestj[h] = better ? (uint32_t)j : bestj[h];
@@ -332,9 +339,10 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
             if (has_next && (uint32_t)lane == nl - 1) {
                 const uint64_t tg = (uint64_t)io.tag_w << 32;
                 gu64* wr = (gu64*)(io.rec_w + 2ull * j);
-                __hip_atomic_store(wr, tg | (uint32_t)(sext_lo(H2[R - 1]) + O[0]), __ATOMIC_RELAXED,
+                // (absolute S: out of the lane frame)
+                __hip_atomic_store(wr, tg | (uint32_t)(sext_lo(H2[R - 1]) + O[0] - dl * lane), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_store(wr + 1, tg | (uint32_t)(sext_hi(H2[R - 1]) + O[1]), __ATOMIC_RELAXED,
+                __hip_atomic_store(wr + 1, tg | (uint32_t)(sext_hi(H2[R - 1]) + O[1] - dl * lane), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             }
         }

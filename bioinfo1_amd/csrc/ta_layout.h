@@ -51,6 +51,20 @@ TA_HD inline int local_max3_offset(uint32_t n, uint32_t m, int ma, int mi, int g
     return (int)(-lo);
 }
 
+// Local flexible fill (ta_flex.hip): the value of a cell is
+//   V = H - ma*j + gap*(j - i) - O + (17*gap - ma)*lane,
+// so that the up candidate is the value above itself and the clamp base of a
+// step (H = 0) is the same in every lane: zu - gap*r for row r of a stripe.
+// Every 64 steps the wave is rebased so that zu = flex_local_c0; between
+// rebases zu moves by (gap - ma) per step.  Values and candidates then lie in
+// [c0 - 64*max(0, ma - gap) - 15*max(0, gap) - 16*mag, c0 + 64*max(0, gap - ma)
+// + 15*max(0, -gap) + hmax + 16*mag]; c0 puts the low end at >= 64.
+TA_HD inline int flex_local_c0(int ma, int mi, int gap) {
+    const int ama = ma < 0 ? -ma : ma, ami = mi < 0 ? -mi : mi, ag = gap < 0 ? -gap : gap;
+    const int mx = ama > ami ? (ama > ag ? ama : ag) : (ami > ag ? ami : ag), mag = mx < 1 ? 1 : mx;
+    return 64 * (ma > gap ? ma - gap : 0) + 15 * (gap > 0 ? gap : 0) + 16 * mag + 64;
+}
+
 // Steps of one pass over an m-column target: m + 63 (lane skew).
 TA_HD inline uint32_t pass_steps(uint32_t m) { return m + kWave - 1; }
 TA_HD inline uint32_t n_passes(uint32_t n) { return (n + kPassRows - 1) / kPassRows; }

@@ -25,17 +25,18 @@ bool flex_fits(int mode, int ma, int mi, int gap) {
     return (kPassRows + 3LL * kWave) * 2 * mag * 2 <= 30000;
 }
 
-// Local mode: the values a wave holds are H - ma*j - O, H in [0, Hmax], kept
-// in [0, 0x7BFF] (ta_flex.hip: the three-input max on f16 bit patterns): the
-// smallest clamp base -ma*j - O starts at C0 = 64|ma| + 16 mag + 64 after
-// every rebase, drifts by up to 64|ma| until the next one, the largest lies
-// 63|ma| above the smallest, candidates one step (mag) below the clamp.
+// Local mode: the values a wave holds lie in [0, 0x7BFF] (ta_flex.hip: the
+// three-input max on f16 bit patterns) -- the frame of ta_layout.h
+// flex_local_c0: above the lane-uniform clamp base zu (kept within 64 steps of
+// drift of c0) by at most 15 rows of |gap| plus H <= hmax, candidates one step
+// (mag) below or above.
 bool flex_local_fits(uint32_t n, uint32_t m, int ma, int mi, int gap) {
     const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
     const long long hmax = (long long)std::min(n, m) * std::max({0LL, (long long)ma, (long long)mi}) +
                            ((long long)n + m) * std::max(0LL, (long long)gap);
-    const long long c0 = 64 * std::llabs(ma) + 16 * mag + 64;
-    return c0 + 127 * std::llabs(ma) + hmax + 64 <= 0x7BFF && hmax + 3LL * kWave * std::llabs(ma) + 8 * mag <= 30000;
+    const long long c0 = flex_local_c0(ma, mi, gap);
+    const long long hi = c0 + 64LL * std::max(0, gap - ma) + 15LL * std::max(0, -gap) + hmax + 16 * mag;
+    return mag <= 64 && hi <= 0x7BFF && hmax + 3LL * kWave * std::llabs(ma) + 8 * mag <= 30000;
 }
 
 // Bounds of the biased 16-bit values of ta_dual.hip (S and every candidate),

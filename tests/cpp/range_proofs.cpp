@@ -5,7 +5,10 @@
 //     plus the offset and the lane frame (z + 16) * lane, for every cell of every row up to n + 15 (the last lane's
 //     padding rows) and every candidate (diag / left / up before the max);
 //   * flex_local_fits (ta_planner.cpp, ta_flex.hip): H itself is bounded by the
-//     planner's hmax for every cell (the rest of that bound is drift arithmetic).
+//     planner's hmax for every cell, and every cell and candidate of the local
+//     flexible fill's frame (ta_layout.h flex_local_c0: zu - gap*r + H with the
+//     row-0 clamp base zu anywhere in its 65-step drift from c0) lies in
+//     [0, 0x7BFF].
 // The DP is the reference's local recurrence (team_alignment.cpp:171-194) on
 // random bytes ('-' in targets, whose gap steps are free).  Prints "ok" or the
 // first violation; exit status 0 / 1.
@@ -76,6 +79,19 @@ int main(int argc, char** argv) {
                     std::printf("flex hmax violated: n=%u m=%u sc=%d,%d,%d H=%ld hmax=%ld\n", n, m, ma, mi, gap, h,
                                 hmax_pl);
                     return 1;
+                }
+                if (flex && i <= n) {
+                    const long c0 = ta::flex_local_c0(ma, mi, gap), r = (long)((i - 1) % 16);
+                    const long zlo = c0 - 65L * std::max(0, ma - gap), zhi = c0 + 65L * std::max(0, gap - ma);
+                    for (long cand : {d, l, u, h}) {
+                        ++checked;
+                        const long lo = zlo - (long)gap * r + cand, hi = zhi - (long)gap * r + cand;
+                        if (lo < 0 || hi > 0x7BFF) {
+                            std::printf("flex local frame violated: n=%u m=%u sc=%d,%d,%d i=%u j=%u cand=%ld [%ld, %ld]\n",
+                                        n, m, ma, mi, gap, i, j, cand, lo, hi);
+                            return 1;
+                        }
+                    }
                 }
             }
     }
