@@ -295,6 +295,14 @@ void check_small_batches() {
                     if (pl.chunks.size() != 1)
                         std::printf("small batch %u x %ux%u type %d flags %u: %zu chunks\n", P, sh[0], sh[1], type, flags,
                                     pl.chunks.size());
+                    // every pair in the packed kernels (an odd one coupled with itself) when it fits
+                    // int16 and is not tiny; band walks (blocked layout) from 8 local pairs up
+                    const bool packed = (uint64_t)sh[0] * sh[1] >= 4096 && ta::fits_int16(type, sh[0], sh[1], 1, -1, -1);
+                    // (n_dual_pairs counts two per couple, a self-coupled pair included)
+                    if (packed) CHECK(pl.singles.empty() && pl.n_dual_pairs == 2 * ((P + 1) / 2));
+                    // (tiny pairs of an even batch still couple with each other; only a lone one stays int32)
+                    const bool all_packed = ta::fits_int16(type, sh[0], sh[1], 1, -1, -1) && (packed || P % 2 == 0);
+                    CHECK(pl.blk == (all_packed && type == ta::kLocal && P >= 8 && flags == 0 && sh[0] + sh[1] <= 6000));
                 }
 }
 
