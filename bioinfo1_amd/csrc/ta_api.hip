@@ -201,7 +201,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         a.slot_off = pl->d_slot_off;
         a.cigar_start = io->cigar_start;
         a.cigar_len = io->cigar_len;
-        a.blk = h.blk ? 1u : 0u;
+        a.blk = h.blk ? (h.ck ? 2u : 1u) : 0u;
         a.pflag = (h.blk && h.walk_group == 64) ? pl->d_pflag : nullptr;
         if (ch.scount) {  // launched first: it may run on the aux stream beside the packed fill
             ta::FillArgs a1 = a;
@@ -313,7 +313,7 @@ int exec_chunk(ta_plan* pl, const ta_device_io* io, hipStream_t s, uint32_t c, b
         t.match = h.match;
         t.mismatch = h.mismatch;
         t.gap = h.gap;
-        t.blk = h.blk ? 1u : 0u;
+        t.blk = h.blk ? (h.ck ? 2u : 1u) : 0u;
         if (h.walk_group == 64) {
             // band walks (one lane per pair), then the pairs of the couples the dual
             // fill handed back ('-' bytes) in the one-pair walk: its list and count
@@ -506,7 +506,7 @@ int ta_plan_fused(const ta_plan* pl) { return pl && pl->h.fused ? 1 : 0; }
 
 int ta_plan_walk(const ta_plan* pl) {
     if (!pl) return -1;
-    return pl->h.walk_group | (pl->h.blk ? 0x100 : 0);
+    return pl->h.walk_group | (pl->h.blk ? 0x100 : 0) | (pl->h.ck ? 0x200 : 0);
 }
 
 int ta_plan_pair_chunks(const ta_plan* pl, uint32_t* chunk_of_pair) {

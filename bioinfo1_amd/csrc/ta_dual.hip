@@ -45,6 +45,18 @@ constexpr int kDualStageL = kDualStage ? kDualStage : 16;  // (array sizes and m
 #ifndef TA_SWAR
 #define TA_SWAR 1
 #endif
+// CK (with TA_DUAL_BLK, a translation unit of its own): checkpoints instead of
+// codes -- each stripe's bottom row every step and its 16 rows every 16 steps
+// (ta_layout.h ck_row_index / ck_col_index), from which the walk recomputes
+// the codes of the cells around its path (ta_walk_ck.hip)
+#ifndef TA_DUAL_CK
+#define TA_DUAL_CK 0
+#endif
+#if defined(TA_DUAL_BLK) && TA_DUAL_CK
+constexpr bool kDualCk = true;
+#else
+constexpr bool kDualCk = false;
+#endif
 
 struct DualIo {
     const uint8_t* Q[2];
@@ -118,6 +130,8 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // every value and candidate of the M3 frame lies in [0, 0x7BFF]
     // (local_max3_offset), so the low half never borrows from the high one
     constexpr bool SW = M3 && TA_SWAR;
+    constexpr bool CK = BLK && kDualCk;
+    constexpr bool CODES = CIGAR && !CK;
     uint32_t GLk = swar_k(LOCAL ? 16 * gap + zstep : 2 * gap - ma), GUGk = swar_k(16 * gap - 1);
     asm volatile("" : "+s"(GLk), "+s"(GUGk));  // SGPR operands (a literal would double the encoding)
     uint32_t ONE = 0x00010001u;
@@ -184,6 +198,33 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     uint32_t* prow1 = CIGAR ? io.ptrs[1] + (BLK ? (uint64_t)pass * io.nb * (kBlkSteps * kWave) : (uint64_t)pass * Tmax * kWave) : nullptr;
     // BLK: the staged kDualStage steps ending at step t (inclusive) -> their
     // place in block t / 16, [b][lane][16], of both pairs
+    // CK: the bottom rows staged for the 16 steps ending at t, split by pair, and
+    // at a block's end (full) all 16 rows after its last step
+    auto ck_flush = [&](uint32_t t, bool full) {
+        const uint32_t b = t >> 4;
+        uint32_t x[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) x[q] = io.cbuf[q * kWave + lane];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+            uint32_t* dr = (h ? prow1 : prow0) + ((uint64_t)b * kWave + (uint32_t)lane) * 8u;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                *reinterpret_cast<uint4*>(dr + 4 * q) =
+                    make_uint4(__builtin_amdgcn_perm(x[8 * q + 1], x[8 * q], sel), __builtin_amdgcn_perm(x[8 * q + 3], x[8 * q + 2], sel),
+                               __builtin_amdgcn_perm(x[8 * q + 5], x[8 * q + 4], sel), __builtin_amdgcn_perm(x[8 * q + 7], x[8 * q + 6], sel));
+            if (full) {
+                uint32_t* dc = dr + (uint64_t)io.nb * kWave * 8u;
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    *reinterpret_cast<uint4*>(dc + 4 * q) =
+                        make_uint4(__builtin_amdgcn_perm(H2[8 * q + 1], H2[8 * q], sel), __builtin_amdgcn_perm(H2[8 * q + 3], H2[8 * q + 2], sel),
+                                   __builtin_amdgcn_perm(H2[8 * q + 5], H2[8 * q + 4], sel), __builtin_amdgcn_perm(H2[8 * q + 7], H2[8 * q + 6], sel));
+            }
+        }
+    };
     auto blk_flush = [&](uint32_t t) {
         const uint64_t at = ((uint64_t)(t >> 4) * kWave + (uint32_t)lane) * kBlkSteps + (t & 15u & ~(uint32_t)(kDualStageL - 1));
 #pragma unroll
@@ -271,7 +312,7 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 uint32_t hv;
                 if constexpr (M3) hv = pk_max3_pos_bc<r & 1>(m1, up, W[r / 2]);  // clamp folded in, :185
                 else hv = LOCAL ? pk_max(pk_max(m1, up), Z) : pk_max(m1, up);
-                if (CIGAR) {
+                if (CODES) {
                     // raw compares (D wins over I in the walk; local walks track the
                     // cost instead of reading a STOP code, ta_device.h WalkSeq)
                     const uint32_t wd = pk_sub_sat(m1, up);    // sign: up > max(diag, left)  (DELETE)
@@ -328,7 +369,9 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                     io.B[j] = (int32_t)bv;
             }
         }
-        if (CIGAR) {
+        if constexpr (CK) {
+            io.cbuf[(t & 15u) * kWave + (uint32_t)lane] = H2[R - 1];  // (flushed by run_steps)
+        } else if (CIGAR) {
             // per pair: [I rows 8-15, I rows 0-7, D rows 8-15, D rows 0-7] (ta_internal.h Code)
             const uint32_t cA = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
             const uint32_t cB = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
@@ -369,8 +412,11 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 step(t + 1, masked_tag);
             }
             if (t < blk) step(t++, masked_tag);
-            if constexpr (BLK && kDualStage)
+            if constexpr (CK) {
+                if ((t & 15u) == 0 || t == steps) ck_flush(t - 1, (t & 15u) == 0);
+            } else if constexpr (BLK && kDualStage) {
                 if ((t & (uint32_t)(kDualStageL - 1)) == 0 || t == steps) blk_flush(t - 1);
+            }
         }
     };
     run_steps(ramp_end, std::true_type{});
@@ -478,7 +524,9 @@ template <int MODE, bool CIGAR, bool BLK = false>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_kernel(FillArgs a) {
     const int lane = threadIdx.x & 63;
     // BLK: code staging per wave (kDualStage steps x 64 lanes x 2 pairs)
-    __shared__ uint32_t cbuf_all[(BLK && kDualStage) ? kWavesPerBlock * 2 * kDualStage * kWave : 1];
+    // (CK: the bottom row of each step, both pairs in one dword)
+    constexpr int kStageDw = kDualCk ? 16 * kWave : 2 * kDualStage * kWave;
+    __shared__ uint32_t cbuf_all[(BLK && kDualStage) ? kWavesPerBlock * kStageDw : 1];
     uint32_t widx, p_only = 0;
     const bool pipe = a.ticket != nullptr;
     if (pipe) {
@@ -509,7 +557,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     io.rec_r = nullptr;
     io.tag_w = io.tag_r = 0;
     io.err = a.err;
-    io.cbuf = cbuf_all + ((BLK && kDualStage) ? (threadIdx.x >> 6) * (2 * kDualStage * kWave) : 0);
+    io.cbuf = cbuf_all + ((BLK && kDualStage) ? (threadIdx.x >> 6) * kStageDw : 0);
     io.nb = blk_count(m);
     bool dash = false, qother = false;
 #pragma unroll
@@ -670,7 +718,9 @@ __global__ void dual_combine_kernel(FillArgs a) {
 }  // namespace
 
 #ifdef TA_DUAL_MODE
-#ifdef TA_DUAL_BLK
+#if defined(TA_DUAL_BLK) && TA_DUAL_CK
+hipError_t launch_dual_ck(const FillArgs& a, hipStream_t s) {
+#elif defined(TA_DUAL_BLK)
 hipError_t launch_dual_blk(const FillArgs& a, hipStream_t s) {
 #else
 template <>
@@ -682,7 +732,7 @@ hipError_t launch_dual_mode<TA_DUAL_MODE, (TA_DUAL_CIGAR != 0)>(const FillArgs& 
                        dim3(kBlock), 0, s, a);
 #else
 #if TA_DUAL_MODE == 1 && TA_DUAL_CIGAR
-    if (a.blk) return launch_dual_blk(a, s);
+    if (a.blk) return a.blk == 2 ? launch_dual_ck(a, s) : launch_dual_blk(a, s);
 #endif
     hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, TA_DUAL_CIGAR != 0>), dual_grid(a.ticket ? a.n_tasks : a.count),
                        dim3(kBlock), 0, s, a);

@@ -65,7 +65,9 @@ struct FillArgs {
     // pass = level (pass-major) or level - (chunk passes - couple passes) (end-aligned)
     uint32_t end_aligned;
     // blocked code layout (ta_layout.h blk_index): the dual fill stages 16 steps
-    // in LDS and writes [block][lane][16 steps]; the int32 fill stores per step
+    // in LDS and writes [block][lane][16 steps]; the int32 fill stores per step.
+    // 2: the dual fill writes checkpoints instead (ta_layout.h ck_row_index; the
+    // int32 fill of handed-back couples still writes blocked codes)
     uint32_t blk;
     // blk plans: per pair, 1 when its couple was handed back ('-' bytes; the
     // band walk leaves it to the fallback walk), written by the dual fill
@@ -102,7 +104,7 @@ struct TraceArgs {
     const uint8_t* tbytes;
     const uint64_t* toff;
     int match, mismatch, gap;
-    uint32_t blk;                // codes in the blocked layout (ta_layout.h blk_index)
+    uint32_t blk;                // codes in the blocked layout (ta_layout.h blk_index); 2: checkpoints (ck_row_index)
     const uint8_t* pflag;        // band walk: pairs to leave to the fallback walk (FillArgs.pflag)
     uint32_t* runs;              // band walks: event words, pair p's at runs + band_runs_off(slot_off[p]) (format_runs_kernel)
     uint32_t* err;               // the plan's error word: band walks set kErrWalkCap
@@ -173,6 +175,11 @@ template <int MODE, bool CIGAR>
 hipError_t launch_dual_mode(const FillArgs& a, hipStream_t s);
 // the local CIGAR dual fill in the blocked code layout (ta_dual.hip, TA_DUAL_BLK)
 hipError_t launch_dual_blk(const FillArgs& a, hipStream_t s);
+// ... and in the checkpoint layout (TA_DUAL_BLK + TA_DUAL_CK; FillArgs.blk == 2)
+hipError_t launch_dual_ck(const FillArgs& a, hipStream_t s);
+// The recomputing local walks of checkpoint plans (ta_walk_ck.hip; TraceArgs.blk == 2),
+// then the fallback walk of the handed-back pairs; format_runs_kernel follows.
+hipError_t launch_walk_ck(const TraceArgs& a, hipStream_t s);
 // Flexible two-pair fill (ta_flex.hip, global / semi-global): a.order holds 2
 // pair ids per wave, the larger n first; both with the same pass count and
 // n mod 16; rebased int16 values, so any length fits.

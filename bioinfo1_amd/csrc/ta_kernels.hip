@@ -1056,7 +1056,12 @@ hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int gro
         return hipGetLastError();
     }
     if (mode == kLocal && group == 64) {  // band walks (blocked layout), one lane per pair
-        hipLaunchKernelGGL(traceback_band_kernel, dim3((a.count + kWave - 1) / kWave), dim3(kWave), 0, s, a);
+        if (a.blk == 2) {  // ... or recomputing walks over checkpoints (ta_walk_ck.hip)
+            const hipError_t e = launch_walk_ck(a, s);
+            if (e != hipSuccess) return e;
+        } else {
+            hipLaunchKernelGGL(traceback_band_kernel, dim3((a.count + kWave - 1) / kWave), dim3(kWave), 0, s, a);
+        }
         hipLaunchKernelGGL(format_runs_kernel, g, b, 0, s, a);
         return hipGetLastError();
     }

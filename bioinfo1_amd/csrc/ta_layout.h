@@ -89,6 +89,26 @@ TA_HD inline uint64_t ptr_dwords_any(uint32_t n, uint32_t m, bool blk) {
 TA_HD inline uint64_t blk_index(uint32_t pass, uint32_t t, uint32_t lane, uint32_t nb) {
     return (((uint64_t)pass * nb + (t >> 4)) * kWave + lane) * kBlkSteps + (t & 15u);
 }
+// Checkpoint layout (ck plans): instead of codes, the local dual
+// fill leaves in a pair's blocked region (nb * 2048 int16 per pass) the packed
+// values a recomputing walk restarts from --
+//   rows: [block][lane][16 steps]  the stripe's bottom row after each step
+//   cols: [block][lane][16 rows]   the stripe's 16 rows after the block's last step
+// (lane l: column t - l + 1 at step t, so block b's column is 16 (b + 1) - l).
+// Both are int16 indexes into the pair's region.
+TA_HD inline uint64_t ck_row_index(uint32_t pass, uint32_t t, uint32_t lane, uint32_t nb) {
+    return ((uint64_t)pass * nb * 2 * kWave + (uint64_t)(t >> 4) * kWave + lane) * kBlkSteps + (t & 15u);
+}
+TA_HD inline uint64_t ck_col_index(uint32_t pass, uint32_t b, uint32_t lane, uint32_t nb, uint32_t r) {
+    return (((uint64_t)pass * 2 + 1) * nb * kWave + (uint64_t)b * kWave + lane) * kBlkSteps + r;
+}
+// H of the cell (i, j) (1-based) from the packed value s the local dual fill
+// held for it in lane l of its pass: s = off + 16 H + (1 - 16 ma) j - i + dl l,
+// with off = local_max3_offset and dl = 17 - 16 ma in the three-input-max frame
+// (off >= 0; ta_dual.hip M3 / UZ), off = dl = 0 otherwise.
+TA_HD inline int ck_decode(int s, int off, int zstep, int dl, int i, int j, int l) {
+    return (s - off - zstep * j + i - dl * l) >> 4;
+}
 // Pass-boundary row (int32 per column) needed only when the query spans > 1 pass.
 TA_HD inline uint64_t bnd_words(uint32_t n, uint32_t m) {
     return n_passes(n) > 1 ? (uint64_t)m + 1 + kWave : 0;

@@ -418,6 +418,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     else if ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) pl.walk_group = 0;
     else if ((flags & kPlanWalk2) || gap < -128 || gap > 127) pl.walk_group = 32;
     else pl.walk_group = 16;
+    pl.ck = pl.blk && pl.walk_group == 64 && !(flags & kPlanNoCk);
     // (Each dual wave walking its own two pairs right after its fill measured
     // slower: config 2 3.10 ms vs 2.19 + 0.65; the walk inherits the fill's
     // register allocation and all waves finish their fills together anyway.)

@@ -23,6 +23,7 @@ constexpr uint32_t kPlanWalk2 = 16u;     // local walks: two pairs per wave (ta_
 constexpr uint32_t kPlanSerialPasses = 32u;  // int32 fill: one wave sweeps all of a pair's passes
 constexpr uint32_t kPlanPassMajor = 64u;     // pass tasks ticketed start-aligned (every pass 0 first)
 constexpr uint32_t kPlanNoBlk = 128u;        // keep the [step][lane] code layout (no band walks)
+constexpr uint32_t kPlanNoCk = 256u;         // blk plans: codes + band walks, not checkpoints + recomputing walks
 
 // Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
@@ -48,6 +49,10 @@ struct Plan {
     // codes in the blocked layout (ta_layout.h blk_index): local plans of short
     // pairs in equal-shape couples only (the band walk's layout)
     bool blk = false;
+    // blk plans walked with gap <= 0: the dual fill leaves checkpoints instead of
+    // codes and the walk recomputes the cells around its path (ta_layout.h
+    // ck_row_index, ta_walk_ck.hip)
+    bool ck = false;
     std::vector<uint32_t> qlen, tlen;
     std::vector<uint32_t> order;    // traceback order (all pairs)
     std::vector<uint32_t> singles;  // int32 fill: pair ids

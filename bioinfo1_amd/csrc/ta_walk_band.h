@@ -198,10 +198,11 @@ __device__ __forceinline__ void bw_runs_out(uint32_t src, uint32_t* dst) {
 }
 
 // The local walks of pairs 64 * blockIdx.x + lane (one wave per block).  One
-// event per walked column to a.runs: the D run's length above bit 2, the move
-// after it in bits 1:0 (0 M, 1 I, 3 none: the run left the stripe); their
-// number to cigar_len (format_runs_kernel merges them into runs and replaces
-// it by the text length).
+// event per walked column to a.runs: the D run's length above bit 16, the move
+// after it in bits 1:0 (0 M, 1 I, 3 none: the run left the stripe) and its
+// count (here 1; the recomputing walk's I runs, ta_walk_ck.hip) in bits 15:2;
+// their number to cigar_len (format_runs_kernel merges them into runs and
+// replaces it by the text length).
 __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t* lds, int lane) {
     const uint32_t k = 64u * blockIdx.x + (uint32_t)lane;
     bool has = k < a.count;
@@ -318,7 +319,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
             // one column: the D run from row rr up (bit planes, ta_internal.h Code:
             // row rr's D at 31 - rr), then the M or I move at the row it stops on
             // (none when the run leaves the stripe at its top); its event is the D
-            // run's length above bit 2, the move in bits 1:0 (3: none)
+            // run's length above bit 16, the move in bits 1:0 (3: none), its count (1) between
             auto column = [&](uint32_t xc, uint32_t tbc, int rr, int& dH, uint32_t& ev, int& nrow, bool& top) {
                 const uint32_t dp = xc >> (31 - rr);
                 const int kd = (int)__builtin_ctz(~dp);  // <= rr + 1
@@ -334,7 +335,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
                 const int sc = (qb == tbc) ? mav : miv;
                 const int mv = top ? 0 : (ib ? gapv : sc);
                 dH = __mul24(kd, gapv) + mv;
-                ev = ((uint32_t)kd << 2) | (top ? 3u : ib);
+                ev = ((uint32_t)kd << 16) | 4u | (top ? 3u : ib);
                 nrow = (top || ib) ? rp : rp - 1;
             };
             bool take = ok, prev_top = false;
@@ -444,7 +445,7 @@ __device__ __forceinline__ void bw_put_run(char* q, uint32_t c, uint32_t op, uin
 
 // One wave per pair of a band-walked chunk: its events (walk order, i.e. the
 // CIGAR's last run first) expanded into items -- the event's D run (when
-// long 1+), then its move (when any) -- and items of one op next to each other
+// long 1+), then its move (when any, count times) -- and items of one op next to each other
 // merged into runs, formatted right to left into the end of its slot, 64
 // events per round (RunWriter's layout, ta_device.h; "1\0" for no move,
 // :145-160).  A run still open at the end of a round is carried into the next.
@@ -481,8 +482,8 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
         const bool act = k < E;
         const uint32_t v = vnext;
         vnext = k + 64u < E ? ev[k + 64u] : 0u;
-        const uint32_t kd = v >> 2, mop = act ? (v & 3u) : 3u;
-        const bool va = kd > 0, vb = mop != 3u;      // item A: D x kd; item B: the move (M / I) x 1
+        const uint32_t kd = v >> 16, bc = (v >> 2) & 0x3FFFu, mop = act ? (v & 3u) : 3u;
+        const bool va = kd > 0, vb = mop != 3u;      // item A: D x kd; item B: the move (M / I) x bc
         const uint32_t first = va ? 2u : mop;        // op of the event's first / last item (3: no item)
         const uint32_t last = vb ? mop : (va ? 2u : 3u);
         // the previous event's last op (lane 0: the carried run's), the next
@@ -494,17 +495,17 @@ __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int 
         const bool ha = va && plast != 2u;                   // A starts a run
         const bool hb = vb && (va || plast != mop);          // B starts a run (always after an A)
         // item prefix sums: lane k's items end at pre_k; the carried count precedes lane 0
-        const uint32_t tot = kd + (vb ? 1u : 0u);
+        const uint32_t tot = kd + (vb ? bc : 0u);
         const uint32_t pre = bw_scan_add(tot + (lane == 0 ? ccnt : 0u));
-        const uint32_t preA = pre - (vb ? 1u : 0u);  // through item A
+        const uint32_t preA = pre - (vb ? bc : 0u);  // through item A
         // the prefix just before the latest run head at or before each lane's end
         // (a max scan: prefixes grow); the carried run's head sits at prefix 0
-        int hv = hb ? (int)(pre - 1u) : (ha ? (int)(preA - kd) : -1);
+        int hv = hb ? (int)(pre - bc) : (ha ? (int)(preA - kd) : -1);
         const int hmax = bw_scan_max(hv);
         const int hprev0 = wave_shr1(0, hmax);
         const int hprev = lane == 0 ? 0 : max(hprev0, 0);  // (lane 0 continues the carry: head at 0)
         const uint32_t sumA = preA - (uint32_t)(ha ? (int)(preA - kd) : hprev);
-        const uint32_t sumB = pre - (uint32_t)(hb ? (int)(pre - 1u) : hprev);
+        const uint32_t sumB = pre - (uint32_t)(hb ? (int)(pre - bc) : hprev);
         // run ends: A before B, or before the next event's first item of another op;
         // lane 63's last item may continue into the next round
         const bool more = lane == 63 && base + 64u < E;  // (lane 63 of a non-final round)

@@ -173,6 +173,8 @@ int ta_align_batch_flags(ta_context* ctx, uint32_t n_pairs, const char* query_by
 #define TA_PLAN_PASS_MAJOR 64u    /* pass-pipelined fills: tickets start-aligned (every pass 0 first), not end-aligned */
 #define TA_PLAN_NO_BLK 128u       /* local plans of equal-shape couples: keep the [step][lane] code layout and the
                                      lane walks instead of the blocked layout and the band walks */
+#define TA_PLAN_NO_CK 256u        /* those plans: the fill writes blocked codes walked by the band walks, instead of
+                                     checkpoints walked by the recomputing walks */
 int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
                    const uint32_t* target_len_host, int type, int match, int mismatch, int gap, int want_cigar,
                    uint64_t workspace_budget, uint32_t flags, ta_plan** out);
@@ -193,7 +195,8 @@ uint32_t ta_plan_flex_pairs(const ta_plan* plan);
 int ta_plan_fused(const ta_plan* plan);
 /* The plan's walk (diagnostics, tests): local walk kind in bits 7:0 (64 band walks,
  * one lane per pair; 32 two pairs per wave; 16 lane walks; 0 one pair per wave),
- * bit 8 set when the codes use the blocked layout. */
+ * bit 8 set when the codes use the blocked layout, bit 9 when the fill leaves
+ * checkpoints instead and the walk recomputes codes around its path. */
 int ta_plan_walk(const ta_plan* plan);
 /* chunk_of_pair[p] = the chunk (0 .. ta_plan_chunks-1) whose launches align pair p
  * (caller-allocated, n_pairs entries).  Diagnostics: which chunk a checked pair ran in. */

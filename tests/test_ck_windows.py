@@ -1,0 +1,125 @@
+"""Host check of the recomputing walk's window logic (ta_walk_ck.hip): the
+walk of checkpoint plans crosses each 16-row stripe in windows that start at
+the stripe's checkpoint column at least kCkLead columns left of the walk
+(checkpoints at columns 16 (b + 1) - l for stripe lane l, or column 0), and
+steps one row at a time -- stop on a cell with H = 0, else the run of I moves
+(trailing ones of the row's I-only bits, stopped at the window's edge), then
+the D or M move out of the row.  Here the same window arithmetic runs on the
+exact DP matrix of the reference recurrence (team_alignment.cpp:171-217) and
+must give the reference walk's path for every pair, including I runs longer
+than a window and D runs across stripes."""
+import numpy as np
+import pytest
+
+LEAD = 17
+
+
+def dp(q, t, ma, mi, gap):
+    n, m = len(q), len(t)
+    H = np.zeros((n + 1, m + 1), np.int64)
+    D = np.zeros((n + 1, m + 1), bool)
+    I = np.zeros((n + 1, m + 1), bool)
+    best, gi, gj = None, 0, 0
+    for i in range(1, n + 1):
+        for j in range(1, m + 1):
+            dg = H[i - 1, j - 1] + (ma if q[i - 1] == t[j - 1] else mi)
+            lf, up = H[i, j - 1] + gap, H[i - 1, j] + gap
+            I[i, j], D[i, j] = lf > dg, up > max(dg, lf)
+            H[i, j] = max(dg, lf, up, 0)
+            if best is None or H[i, j] > best:
+                best, gi, gj = H[i, j], i, j
+    return H, D, I, gi, gj
+
+
+def reference_walk(H, D, I, i, j):
+    out = []
+    while H[i, j] > 0:
+        if D[i, j]:
+            out.append("D")
+            i -= 1
+        elif I[i, j]:
+            out.append("I")
+            j -= 1
+        else:
+            out.append("M")
+            i, j = i - 1, j - 1
+    return "".join(reversed(out))
+
+
+def window_walk(H, D, I, i, j, q, t, sc):
+    """The kernel's walk: window columns and row steps; H only as the 0 test.
+    Each window is first recomputed from its checkpoint column and the stripe
+    above's bottom row alone, as the kernel does, and must equal the matrix."""
+    out = []
+    while True:
+        g, r = (i - 1) >> 4, (i - 1) & 15
+        lane = g & 63
+        e = j - LEAD + lane
+        c0 = max((e >> 4) * 16 - lane, 0) if e >= 16 else 0
+        W = j - c0
+        assert 1 <= W <= LEAD + 15 and c0 >= 0, (W, j, c0)
+        ma, mi, gap = sc
+        hw = {}
+        for a in range(16 * g + 1, min(16 * g + 16, H.shape[0] - 1) + 1):
+            for b in range(c0 + 1, j + 1):
+                get = lambda u, v: H[u, v] if (u == 16 * g or v == c0) else hw[(u, v)]  # noqa: E731
+                s = ma if q[a - 1] == t[b - 1] else mi
+                hw[(a, b)] = max(get(a - 1, b - 1) + s, get(a, b - 1) + gap, get(a - 1, b) + gap, 0)
+                assert hw[(a, b)] == H[a, b], (a, b)
+        # row words: column x at bit W - x; I-only, D, zero
+        rows = {}
+        for rr in range(r + 1):
+            a = 16 * g + rr + 1
+            io = dd = zz = 0
+            for x in range(1, W + 1):
+                b, bit = c0 + x, 1 << (W - x)
+                io |= bit if (I[a, b] and not D[a, b]) else 0
+                dd |= bit if D[a, b] else 0
+                zz |= bit if H[a, b] == 0 else 0
+            rows[rr] = (io, dd, zz)
+        rr, x, stop = r, W, False
+        while rr >= 0 and x >= 1:
+            io, dd, zz = rows[rr]
+            pos = W - x
+            if (zz >> pos) & 1:
+                stop = True
+                break
+            v, run = io >> pos, 0
+            while v & 1 and run < x:
+                v >>= 1
+                run += 1
+            out += ["I"] * run
+            x -= run
+            if x == 0:
+                break
+            if (dd >> (pos + run)) & 1:
+                out.append("D")
+            else:
+                out.append("M")
+                x -= 1
+            rr -= 1
+        i, j = 16 * g + rr + 1, c0 + x
+        if stop or i < 1 or j < 1:
+            return "".join(reversed(out))
+
+
+@pytest.mark.parametrize("sc", [(1, -1, -1), (2, -3, -1), (3, 4, 0), (4, -1, -2), (1, 0, -1)])
+def test_window_walk_matches_reference(sc):
+    rng = np.random.default_rng(0xC4 + sc[0] * 31 + sc[2])
+    al = b"ACGT"
+    # (the last two: stripes of lanes >= 16, whose first checkpoints precede column 1)
+    for k, (n, m) in enumerate([(70, 90), (120, 60), (40, 130), (100, 100), (90, 75), (33, 140), (400, 45), (700, 30)]):
+        q = bytes(al[v] for v in rng.integers(4, size=n))
+        t = bytes(al[v] for v in rng.integers(4, size=m))
+        if k % 3 == 1:  # a long insertion in the target: an I run longer than a window
+            cut = n // 2
+            t = (q[:cut] + b"N" * 45 + q[cut:])[:m] if m > cut + 45 else t
+        if k % 3 == 2:  # a deletion: a D run across stripes
+            cut = min(n, m) // 3
+            q = (t[:cut] + b"N" * 35 + t[cut:])[:n]
+        if k >= 6:  # the target is a piece of the query deep down: the path reaches column 1 there
+            t = q[n - m - 20:n - 20]
+        H, D, I, gi, gj = dp(q, t, *sc)
+        if H[gi, gj] <= 0:
+            continue
+        assert window_walk(H, D, I, gi, gj, q, t, sc) == reference_walk(H, D, I, gi, gj), (sc, k)

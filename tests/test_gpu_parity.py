@@ -9,7 +9,7 @@ import pytest
 from conftest import DIGESTS, ROOT, STRIDED, cigar_digest, digest_batch, load_digest, run_plan
 
 from bioinfo1_amd import synth
-from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_BLK, TA_PLAN_NO_FLEX, TA_PLAN_SERIAL_PASSES, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2, Aligner, DevicePlan,
+from bioinfo1_amd.align import (TA_PLAN_INT32_ONLY, TA_PLAN_NO_BLK, TA_PLAN_NO_CK, TA_PLAN_NO_FLEX, TA_PLAN_SERIAL_PASSES, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2, Aligner, DevicePlan,
                                 align)
 from oracle.pyoracle import Oracle
 
@@ -483,15 +483,63 @@ def test_band_walk(aligner, oracle, case):
         pairs += [(rb.query(p), rb.target(p)) for p in range(rb.n_pairs)]
     b = synth.from_pairs(pairs)
     plan = DevicePlan(aligner, b, 1, *sc, True)
-    assert plan.blk and plan.walk == walk, (plan.blk, plan.walk)
+    # (walked with gap <= 0: checkpoints + recomputing walks by default, ta_walk_ck.hip)
+    assert plan.blk and plan.walk == walk and plan.ck == (walk == 64), (plan.blk, plan.walk, plan.ck)
     plan.close()
     want = oracle.align_batch(b, 1, *sc, True)
-    for flags in (0, TA_PLAN_NO_BLK):
+    for flags in (0, TA_PLAN_NO_CK, TA_PLAN_NO_BLK):
         got = run_plan(aligner, b, 1, sc, True, flags)
         np.testing.assert_array_equal(got.scores, want.scores)
         np.testing.assert_array_equal(got.target_begins, want.target_begins)
         for p in range(b.n_pairs):
             assert got.cigar(p) == want.cigar(p), (case, flags, p, b.qlen[p], b.tlen[p])
+
+
+CK_SCORES = [(1, -1, -1), (2, -3, -1), (1, -2, -3), (3, 4, 0), (5, -4, -3), (1, 0, -1), (4, -1, -2)]
+
+
+@pytest.mark.parametrize("sc", CK_SCORES)
+def test_ck_walk(aligner, oracle, sc):
+    """Recomputing walks over checkpoints (ta_walk_ck.hip) against the oracle:
+    an odd number of couples of each shape (a pair coupled with itself), one
+    to three query passes, and paths with long I runs (more than a window of
+    32 columns) and long D runs (across stripes and a pass edge) -- inserted
+    blocks that match nothing -- beside random and related pairs."""
+    rng = np.random.default_rng(0xC4EC + 7 * sc[0] - sc[1])
+    al = np.frombuffer(b"ACGT", np.uint8)
+    rnd = lambda k: al[rng.integers(4, size=k)].tobytes()  # noqa: E731
+    pairs = []
+    # shapes within the dual fill's int16 frame for these scores (ta_planner.cpp fits_int16)
+    hs, mag = max(sc[0], sc[1], 1), max(abs(sc[0]), abs(sc[1]), abs(sc[2]), 1)
+    mcap, scap = (28900 - 32 * mag) // (16 * sc[0] - 1), (31000 - 32 * mag) // (16 * hs)
+    for n, m, cnt in ((300, 280, 9), (1030, 990, 5), (2100, 700, 3), (40, 1200, 3), (1500, 64, 3)):
+        m = min(m, mcap)
+        if min(n, m) > scap:
+            m = scap
+        for k in range(cnt):
+            core = rnd(min(n, m) - 200 if min(n, m) > 400 else min(n, m) // 2)
+            gapb = b"N" * (40 + 23 * k)
+            if k % 3 == 0:  # an insertion in the target: an I run
+                q, t = core, core[: len(core) // 2] + gapb + core[len(core) // 2:]
+            elif k % 3 == 1:  # a deletion: a D run
+                q, t = core[: len(core) // 3] + gapb + core[len(core) // 3:], core
+            else:
+                q, t = rnd(n), rnd(m)
+            q, t = (q + rnd(max(0, n - len(q))))[:n], (t + rnd(max(0, m - len(t))))[:m]
+            pairs.append((q, t))
+    L = min(1000, mcap, scap)
+    rb = synth.related_batch(9, L, L, seed=0xC4ED)
+    pairs += [(rb.query(p), rb.target(p)) for p in range(rb.n_pairs)]
+    b = synth.from_pairs(pairs)
+    plan = DevicePlan(aligner, b, 1, *sc, True)
+    assert plan.blk and plan.ck and plan.walk == 64, (plan.blk, plan.ck, plan.walk)
+    plan.close()
+    want = oracle.align_batch(b, 1, *sc, True)
+    got = run_plan(aligner, b, 1, sc, True, 0)
+    np.testing.assert_array_equal(got.scores, want.scores)
+    np.testing.assert_array_equal(got.target_begins, want.target_begins)
+    for p in range(b.n_pairs):
+        assert got.cigar(p) == want.cigar(p), (sc, p, b.qlen[p], b.tlen[p])
 
 
 def test_local_walk_long_runs(aligner, oracle):
