@@ -34,9 +34,15 @@ namespace {
 
 constexpr int kCkLead = 17;            // columns a window reaches left of the walk's column, at least
 constexpr int kCkMaxW = kCkLead + 15;  // the widest window (checkpoints 16 columns apart)
-constexpr int kCkLanes = 8;            // lanes per pair, two rows of the stripe each
+// lanes per pair: 16 (a row of the stripe each) or 8 (two rows each)
+#ifndef TA_CK_LANES
+#define TA_CK_LANES 16
+#endif
+constexpr int kCkLanes = TA_CK_LANES;
+constexpr int kCkRows = 16 / kCkLanes;      // rows per lane
 constexpr int kCkPairs = kWave / kCkLanes;  // pairs per wave
-// sweep steps: W + 7 <= kCkMaxW + 7, run in blocks of 8; two 32-bit words per row keep them all
+static_assert(kCkLanes == 8 || kCkLanes == 16, "lanes per pair");
+// sweep steps: W + lanes - 1, run in blocks of 8; two 32-bit words per row keep them all
 constexpr int kCkMaxSteps = (kCkMaxW + kCkLanes - 1 + 7) / 8 * 8;
 static_assert(kCkMaxSteps <= 64, "a window's steps fit a 64-bit row word");
 
@@ -64,7 +70,7 @@ __device__ unsigned long long ck_prof[8];
 
 __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
     __shared__ CkGroup groups[kWavesPerBlock * kCkPairs];
-    const int lane = (int)threadIdx.x & 63, lg = lane & (kCkLanes - 1), ra = 2 * lg;  // rows ra, ra + 1
+    const int lane = (int)threadIdx.x & 63, lg = lane & (kCkLanes - 1), ra = kCkRows * lg;  // rows ra (, ra + 1)
     CkGroup& G = groups[threadIdx.x / kCkLanes];
     const uint32_t slot = (blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kCkPairs + (uint32_t)(lane / kCkLanes);
     bool has = slot < a.count;
@@ -117,8 +123,9 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
         // every load of the window first (one wait for all), then the decodes
         constexpr int kTopQ = (kCkMaxW + kCkLanes) / kCkLanes, kTbQ = kCkMaxW / kCkLanes;
         const bool hl_ok = live && c0 > 0 && ir <= (int)n;
-        // (rows ra, ra + 1: two adjacent int16 of the checkpoint, one aligned dword)
-        const uint32_t v2 = hl_ok ? *reinterpret_cast<const uint32_t*>(P + ck_col_index(pass, (uint32_t)(e >> 4) - 1u, l, nb, ra)) : 0u;
+        // (two rows: two adjacent int16 of the checkpoint, one aligned dword)
+        const uint32_t ck_at = hl_ok ? (uint32_t)ck_col_index(pass, (uint32_t)(e >> 4) - 1u, l, nb, ra) : 0u;
+        const uint32_t v2 = !hl_ok ? 0u : (kCkRows == 2 ? *reinterpret_cast<const uint32_t*>(P + ck_at) : (uint32_t)P[ck_at]);
         int tr[kTopQ];
         uint32_t tbv[kTbQ];
 #pragma unroll
@@ -131,9 +138,13 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
             const int x = 1 + lg + kCkLanes * q;
             tbv[q] = (live && x <= W) ? T[c0 + x - 1] : 0u;
         }
-        const uint32_t qa = (live && ir <= (int)n) ? Q[ir - 1] : 0u, qb = (live && ir < (int)n) ? Q[ir] : 0u;
-        const int hla = hl_ok ? ck_decode((int)(int16_t)(v2 & 0xFFFFu), off, zstep, dl, ir, c0, l) : 0;  // H(ir, c0)
-        const int hlb = hl_ok ? ck_decode((int)(int16_t)(v2 >> 16), off, zstep, dl, ir + 1, c0, l) : 0;
+        uint32_t qv[kCkRows];
+        int gl[kCkRows];  // own H + gap: the next column's left candidates (H(row, c0) first)
+#pragma unroll
+        for (int h = 0; h < kCkRows; ++h) {
+            qv[h] = (live && ir + h <= (int)n) ? Q[ir - 1 + h] : 0u;
+            gl[h] = (hl_ok ? ck_decode((int)(int16_t)(v2 >> (16 * h)), off, zstep, dl, ir + h, c0, l) : 0) + gap;
+        }
 #pragma unroll
         for (int q = 0; q < kTopQ; ++q) {
             const int x = lg + kCkLanes * q, col = c0 + x;
@@ -144,24 +155,26 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
             const int x = 1 + lg + kCkLanes * q;
             if (live && x <= W) G.tb[16 + x] = (uint8_t)tbv[q];
         }
-        G.q[ra] = (uint8_t)qa;
-        G.q[ra + 1] = (uint8_t)qb;
+#pragma unroll
+        for (int h = 0; h < kCkRows; ++h) G.q[ra + h] = (uint8_t)qv[h];
         ck_wave_sync();
 
-        // ---- the sweep: step k, lane lg computes column x = k - lg + 1 of rows ra, ra + 1
-        const int K = ((wave_max(W > 0 ? W + (r >> 1) : 0) + 7) >> 3) << 3;
+        // ---- the sweep: step k, lane lg computes column x = k - lg + 1 of its rows
+        const int K = ((wave_max(W > 0 ? W + r / kCkRows : 0) + 7) >> 3) << 3;
         CK_T(t1);
         CK_ACC(0, t1 - t0);
         CK_ACC(4, 1);
         CK_ACC(6, K);
-        int ga = hla + gap, gb = hlb + gap;  // own H + gap: the next column's left candidates
         int upp = G.top[0];  // the previous step's up candidate of row ra (lane 0: H(16g, c0) + gap)
-        uint32_t da0 = 0, da1 = 0, ia0 = 0, ia1 = 0, za0 = 0, za1 = 0;
-        uint32_t db0 = 0, db1 = 0, ib0 = 0, ib1 = 0, zb0 = 0, zb1 = 0;
+        uint32_t db[kCkRows][2], ib[kCkRows][2], zb[kCkRows][2];
+#pragma unroll
+        for (int h = 0; h < kCkRows; ++h)
+            for (int w = 0; w < 2; ++w) db[h][w] = ib[h][w] = zb[h][w] = 0u;
         const uint8_t* tbl = &G.tb[17 - lg];
         const bool first = lg == 0;
         auto block = [&](int kb, auto ramp_tag, auto hi_tag) {
-            constexpr bool RAMP = decltype(ramp_tag)::value, HI = decltype(hi_tag)::value;
+            constexpr bool RAMP = decltype(ramp_tag)::value;
+            constexpr int HW = decltype(hi_tag)::value ? 1 : 0;
             int tv[8], bv[8];
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
@@ -170,57 +183,50 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
             }
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-                // row ra: up from the lane above's row ra - 1 (row_shr:1; a group's first lane: the top row)
-                const int dpp = __builtin_amdgcn_update_dpp(tv[s], gb, 0x111, 0xF, 0xF, false);
-                const int upc = first ? tv[s] : dpp;
-                const int dga = upp + ((uint32_t)bv[s] == qa ? sA : sB);
-                const int m1a = max(dga, ga);
-                const int hna = max(max(m1a, upc), 0);
-                const int gan = hna + gap;
-                // row ra + 1: up = row ra's new value, diagonal = row ra's previous one
-                const int dgb = ga + ((uint32_t)bv[s] == qb ? sA : sB);
-                const int m1b = max(dgb, gb);
-                const int hnb = max(max(m1b, gan), 0);
-                // signs: D, I, H = 0
-                const uint32_t dsa = (uint32_t)(m1a - upc), isa = (uint32_t)(dga - ga), zsa = (uint32_t)(hna - 1);
-                const uint32_t dsb = (uint32_t)(m1b - gan), isb = (uint32_t)(dgb - gb), zsb = (uint32_t)(hnb - 1);
-                if constexpr (HI) {
-                    da1 = __builtin_amdgcn_alignbit(da1, dsa, 31);
-                    ia1 = __builtin_amdgcn_alignbit(ia1, isa, 31);
-                    za1 = __builtin_amdgcn_alignbit(za1, zsa, 31);
-                    db1 = __builtin_amdgcn_alignbit(db1, dsb, 31);
-                    ib1 = __builtin_amdgcn_alignbit(ib1, isb, 31);
-                    zb1 = __builtin_amdgcn_alignbit(zb1, zsb, 31);
-                } else {
-                    da0 = __builtin_amdgcn_alignbit(da0, dsa, 31);
-                    ia0 = __builtin_amdgcn_alignbit(ia0, isa, 31);
-                    za0 = __builtin_amdgcn_alignbit(za0, zsa, 31);
-                    db0 = __builtin_amdgcn_alignbit(db0, dsb, 31);
-                    ib0 = __builtin_amdgcn_alignbit(ib0, isb, 31);
-                    zb0 = __builtin_amdgcn_alignbit(zb0, zsb, 31);
+                // the first row: up from the lane above's last row (row_shr:1; a
+                // group's first lane: the top row), diagonal = the previous step's up
+                const int dpp = __builtin_amdgcn_update_dpp(tv[s], gl[kCkRows - 1], 0x111, 0xF, 0xF, false);
+                int up = (kCkLanes == 16 || !first) ? dpp : tv[s];
+                int dg = upp + ((uint32_t)bv[s] == qv[0] ? sA : sB);
+                upp = up;
+                int gn[kCkRows];
+#pragma unroll
+                for (int h = 0; h < kCkRows; ++h) {
+                    if (h) {  // the next row: up = the row above's new value, diagonal = its previous one
+                        dg = gl[h - 1] + ((uint32_t)bv[s] == qv[h] ? sA : sB);
+                        up = gn[h - 1];
+                    }
+                    const int m1 = max(dg, gl[h]);
+                    const int hn = max(max(m1, up), 0);
+                    gn[h] = hn + gap;
+                    // signs: D, I, H = 0
+                    db[h][HW] = __builtin_amdgcn_alignbit(db[h][HW], (uint32_t)(m1 - up), 31);
+                    ib[h][HW] = __builtin_amdgcn_alignbit(ib[h][HW], (uint32_t)(dg - gl[h]), 31);
+                    zb[h][HW] = __builtin_amdgcn_alignbit(zb[h][HW], (uint32_t)(hn - 1), 31);
                 }
                 if (!RAMP || kb + s >= lg) {
-                    ga = gan;
-                    gb = hnb + gap;
+#pragma unroll
+                    for (int h = 0; h < kCkRows; ++h) gl[h] = gn[h];
                 }
-                upp = upc;
             }
         };
         for (int kb = 0; kb < K; kb += 8) {
-            if (kb < 8) block(kb, std::true_type{}, std::false_type{});
+            if (kb < kCkLanes) block(kb, std::true_type{}, std::false_type{});
             else if (kb < 32) block(kb, std::false_type{}, std::false_type{});
             else block(kb, std::false_type{}, std::true_type{});
         }
         // step k at bit K - 1 - k of the 64-bit row; column x = k - lg + 1 at bit W - x of
         // its window word (column 0, bit W, cleared: an I run stops at the window's edge)
         const uint32_t sh = (uint32_t)max(K - lg - W, 0), wmask = W >= 32 ? 0xFFFFFFFFu : (1u << W) - 1u;
-        auto word = [&](uint32_t lo, uint32_t hi) -> uint32_t {
-            const uint64_t u = K > 32 ? ((uint64_t)lo << (K - 32)) | hi : (uint64_t)lo;
+        auto word = [&](const uint32_t (&v)[2]) -> uint32_t {
+            const uint64_t u = K > 32 ? ((uint64_t)v[0] << (K - 32)) | v[1] : (uint64_t)v[0];
             return (uint32_t)(u >> sh) & wmask;
         };
-        const uint32_t wda = word(da0, da1), wdb = word(db0, db1);
-        G.row[ra] = make_uint4(word(ia0, ia1) & ~wda, wda, word(za0, za1), 0u);
-        G.row[ra + 1] = make_uint4(word(ib0, ib1) & ~wdb, wdb, word(zb0, zb1), 0u);
+#pragma unroll
+        for (int h = 0; h < kCkRows; ++h) {
+            const uint32_t wd = word(db[h]);
+            G.row[ra + h] = make_uint4(word(ib[h]) & ~wd, wd, word(zb[h]), 0u);
+        }
         ck_wave_sync();
 
         // ---- the walk across the window, one row per step: stop on a cell with
@@ -229,29 +235,41 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
         // row -- or, when the run reaches column c0, on in the next window.  The
         // loop keeps only what the next step depends on and lists each step's
         // record; the events are made from the records afterwards, in parallel.
+        // (flags as 0 / 1 integers: compares into lane masks and back cost the
+        // loop more than the arithmetic)
         int rr = r, x = W;
         uint32_t nrec = 0;
         const bool room = nev + 2u * (uint32_t)(r + 1) <= cap;  // (<= 2 events per row step)
-        bool wl = live && room, done = false;
+        uint32_t wl = (live && room) ? 1u : 0u, zdone = 0;
         CK_T(t2);
         CK_ACC(1, t2 - t1);
-        uint4 wnext = G.row[rr & 15];
-        while (ballot(wl)) {
-            CK_ACC(5, 1);
-            const uint4 w4 = wnext;
-            wnext = G.row[(rr - 1) & 15];  // (the row a move up reaches: read one step ahead)
+        // Two steps per loop iteration with the row words read one step ahead
+        // into alternating registers (a single one became a copy at the loop's
+        // end, which waited for the read).
+        auto row_step = [&](const uint4& w4) {
             const uint32_t pos = (uint32_t)(W - x);
-            const bool zero = (w4.z >> pos) & 1u;
+            const uint32_t zero = (w4.z >> pos) & 1u;
             const uint32_t run = min((uint32_t)__builtin_ctzll((uint64_t)~(w4.x >> pos) | (1ull << 32)), (uint32_t)x);
-            const int x1 = x - (int)run;
-            const bool edge = x1 == 0, dmove = (w4.y >> ((pos + run) & 31u)) & 1u;
-            const bool go = wl && !zero, mv = go && !edge;
-            G.rec[nrec & 15] = run | (dmove ? 0x100u : 0u) | (edge ? 0x200u : 0u);
-            nrec += go ? 1u : 0u;
-            x = go ? (edge ? 0 : x1 - (dmove ? 0 : 1)) : x;
-            rr = mv ? rr - 1 : rr;
-            done = done || (wl && zero);
-            wl = mv && rr >= 0 && x >= 1;
+            const uint32_t x1 = (uint32_t)x - run;
+            const uint32_t edge = (x1 - 1u) >> 31, dmove = (w4.y >> ((pos + run) & 31u)) & 1u;  // (x1 >= 0)
+            const uint32_t go = wl & (zero ^ 1u), mv = go & (edge ^ 1u);
+            G.rec[nrec & 15] = run | (dmove << 8) | (edge << 9);
+            nrec += go;
+            x -= (int)(go * run + (mv & (dmove ^ 1u)));
+            rr -= (int)mv;
+            zdone |= wl & zero;
+            wl = mv & ((uint32_t)~rr >> 31) & ((uint32_t)(x - 1) >> 31 ^ 1u);  // rr >= 0, x >= 1
+        };
+        uint4 wa = G.row[rr & 15], wb;
+        while (ballot(wl != 0u)) {
+            CK_ACC(5, 1);
+            wb = G.row[(rr - 1) & 15];  // (the row a move up reaches)
+            __builtin_amdgcn_sched_barrier(0);  // (issued here, not sunk to its use)
+            row_step(wa);
+            if (!ballot(wl != 0u)) break;
+            wa = G.row[(rr - 1) & 15];
+            __builtin_amdgcn_sched_barrier(0);
+            row_step(wb);
         }
         ck_wave_sync();
         // events of the records, two per lane: an I run (with the run carried from
@@ -303,7 +321,7 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
                 kI = 0;
             }
             ++windows;
-            done = done || i < 1 || j < 1;  // row 0 / column 0: H = 0
+            const bool done = zdone || i < 1 || j < 1;  // row 0 / column 0: H = 0
             live = !done && room && windows <= n + m + 16u;
             H = done ? 0 : H;
         }

@@ -15,7 +15,9 @@ al = Aligner(0)
 plan = DevicePlan(al, b, 1, 1, -1, -1, True)
 L = lib()
 buf = (C.c_ulonglong * 8)()
-waves = (10000 + 7) // 8
+import os
+lanes = int(os.environ.get("CK_LANES", "16"))
+waves = (10000 + 64 // lanes - 1) // (64 // lanes)
 for it in range(3):
     L.ta_ck_prof(buf, 1)
     plan.run()

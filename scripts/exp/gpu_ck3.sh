@@ -1,0 +1,4 @@
+set -u
+bash scripts/exp/ck_prof.sh || exit 1
+bash scripts/exp/gpu_ck.sh || exit 1
+bash scripts/exp/bench_variants.sh "--steps 10 --warmup 3" ck8
