@@ -29,7 +29,7 @@ LIB_PATH = os.path.join(HERE, "libteam_alignment.so")
 TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY, TA_ERR_RANGE, TA_ERR_UNSERVED = range(8)
 # ta_plan_create flags (include/team_align_c.h): kernel selection, same results
 TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2 = 1, 2, 4, 8, 16
-TA_PLAN_SERIAL_PASSES, TA_PLAN_PASS_MAJOR, TA_PLAN_NO_BLK, TA_PLAN_NO_CK = 32, 64, 128, 256
+TA_PLAN_SERIAL_PASSES, TA_PLAN_PASS_MAJOR, TA_PLAN_NO_BLK, TA_PLAN_NO_CK, TA_PLAN_CK = 32, 64, 128, 256, 512
 
 
 class AlignmentType(enum.IntEnum):

@@ -418,7 +418,17 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     else if ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) pl.walk_group = 0;
     else if ((flags & kPlanWalk2) || gap < -128 || gap > 127) pl.walk_group = 32;
     else pl.walk_group = 16;
-    pl.ck = pl.blk && pl.walk_group == 64 && !(flags & kPlanNoCk);
+    // Checkpoints save the fill ~0.3 of its time but the recomputing walk is a
+    // longer chain per pair than the band walk (one window per 16 rows): they pay
+    // once the cells per unit of the longest path pass ~2.5e6 (1 kb pairs: from
+    // ~5,000 pairs on; 8 to 4,096 measured slower, profiles/bench/r05_ck_batches.txt).
+    uint64_t cells = 0, longest = 1;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        cells += (uint64_t)qlen[p] * tlen[p];
+        longest = std::max<uint64_t>(longest, (uint64_t)qlen[p] + tlen[p]);
+    }
+    pl.ck = pl.blk && pl.walk_group == 64 && !(flags & kPlanNoCk) &&
+            ((flags & kPlanCk) || cells >= 2500000ull * longest);
     // (Each dual wave walking its own two pairs right after its fill measured
     // slower: config 2 3.10 ms vs 2.19 + 0.65; the walk inherits the fill's
     // register allocation and all waves finish their fills together anyway.)

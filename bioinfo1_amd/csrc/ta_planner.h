@@ -24,6 +24,7 @@ constexpr uint32_t kPlanSerialPasses = 32u;  // int32 fill: one wave sweeps all 
 constexpr uint32_t kPlanPassMajor = 64u;     // pass tasks ticketed start-aligned (every pass 0 first)
 constexpr uint32_t kPlanNoBlk = 128u;        // keep the [step][lane] code layout (no band walks)
 constexpr uint32_t kPlanNoCk = 256u;         // blk plans: codes + band walks, not checkpoints + recomputing walks
+constexpr uint32_t kPlanCk = 512u;           // blk plans: checkpoints + recomputing walks at any batch size
 
 // Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
@@ -49,9 +50,9 @@ struct Plan {
     // codes in the blocked layout (ta_layout.h blk_index): local plans of short
     // pairs in equal-shape couples only (the band walk's layout)
     bool blk = false;
-    // blk plans walked with gap <= 0: the dual fill leaves checkpoints instead of
-    // codes and the walk recomputes the cells around its path (ta_layout.h
-    // ck_row_index, ta_walk_ck.hip)
+    // blk plans walked with gap <= 0 whose fill is long against their walks: the
+    // dual fill leaves checkpoints instead of codes and the walk recomputes the
+    // cells around its path (ta_layout.h ck_row_index, ta_walk_ck.hip)
     bool ck = false;
     std::vector<uint32_t> qlen, tlen;
     std::vector<uint32_t> order;    // traceback order (all pairs)

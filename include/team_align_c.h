@@ -173,8 +173,9 @@ int ta_align_batch_flags(ta_context* ctx, uint32_t n_pairs, const char* query_by
 #define TA_PLAN_PASS_MAJOR 64u    /* pass-pipelined fills: tickets start-aligned (every pass 0 first), not end-aligned */
 #define TA_PLAN_NO_BLK 128u       /* local plans of equal-shape couples: keep the [step][lane] code layout and the
                                      lane walks instead of the blocked layout and the band walks */
-#define TA_PLAN_NO_CK 256u        /* those plans: the fill writes blocked codes walked by the band walks, instead of
-                                     checkpoints walked by the recomputing walks */
+#define TA_PLAN_NO_CK 256u        /* those plans: the fill writes blocked codes walked by the band walks, never
+                                     checkpoints walked by the recomputing walks (the default for large batches) */
+#define TA_PLAN_CK 512u           /* those plans: checkpoints and recomputing walks at any batch size */
 int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
                    const uint32_t* target_len_host, int type, int match, int mismatch, int gap, int want_cigar,
                    uint64_t workspace_budget, uint32_t flags, ta_plan** out);

@@ -25,5 +25,5 @@ for it in range(3):
     L.ta_ck_prof(buf, 1)
     v = list(buf)
     print("iter", it, "related" if related else "uniform",
-          "per wave: setup %.0f sweep %.0f walk %.0f total %.0f cycles | windows %.1f, walk iterations %.1f, mean K %.1f" %
-          (v[0] / waves, v[1] / waves, v[2] / waves, v[3] / waves, v[4] / waves, v[5] / waves, v[6] / max(v[4], 1)))
+          "per wave: setup %.0f sweep %.0f walk %.0f total %.0f cycles | windows %.1f, walk iterations %.1f; counters 6, 7: %d %d" %
+          (v[0] / waves, v[1] / waves, v[2] / waves, v[3] / waves, v[4] / waves, v[5] / waves, v[6], v[7]))

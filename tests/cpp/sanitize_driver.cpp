@@ -285,7 +285,7 @@ void check_small_batches() {
     for (const auto& sh : shapes)
         for (uint32_t P : {1u, 2u, 3u, 8u, 16u, 33u})
             for (int type = 0; type < 3; ++type)
-                for (uint32_t flags : {0u, 128u, 256u}) {  // 128: TA_PLAN_NO_BLK, 256: TA_PLAN_NO_CK
+                for (uint32_t flags : {0u, 128u, 256u, 512u}) {  // TA_PLAN_NO_BLK, TA_PLAN_NO_CK, TA_PLAN_CK
                     std::vector<uint32_t> q(P, sh[0]), t(P, sh[1]);
                     const uint64_t budget = std::max<uint64_t>(ta::host_batch_code_bytes(P, q.data(), t.data(), 4), 1);
                     ta::Plan pl;
@@ -303,8 +303,8 @@ void check_small_batches() {
                     // (tiny pairs of an even batch still couple with each other; only a lone one stays int32)
                     const bool all_packed = ta::fits_int16(type, sh[0], sh[1], 1, -1, -1) && (packed || P % 2 == 0);
                     CHECK(pl.blk == (all_packed && type == ta::kLocal && P >= 8 && flags != 128u && sh[0] + sh[1] <= 6000));
-                    // checkpoints and recomputing walks unless TA_PLAN_NO_CK (gap -1 <= 0)
-                    CHECK(pl.ck == (pl.blk && flags == 0));
+                    // checkpoints and recomputing walks: small batches only with TA_PLAN_CK (gap -1 <= 0)
+                    CHECK(pl.ck == (pl.blk && flags == 512u));
                 }
 }
 
