@@ -575,6 +575,8 @@ def dominant_kernel(plan, mode, cigar, affine):
     if plan.flex_pairs and plan.flex_pairs * 2 >= plan.P:
         return f"flex_fill_kernel<{mode}, {c}>"
     if plan.dual_pairs * 2 >= plan.P:
+        if cigar and getattr(plan, "ck", False):
+            return "dual_fill_ck_kernel"  # (checkpoints instead of codes)
         return f"dual_fill_kernel<{mode}, {c}, {'true' if (cigar and plan.blk) else 'false'}>"
     return f"fill_kernel<{mode}, {c}, false>"
 

@@ -521,7 +521,7 @@ constexpr uint32_t kDualSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to 
 // each wave writes its pass's PassOut and dual_combine_kernel folds them.
 // Otherwise one wave per couple sweeps its passes.
 template <int MODE, bool CIGAR, bool BLK = false>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_kernel(FillArgs a) {
+__device__ __forceinline__ void dual_fill_body(const FillArgs& a) {
     const int lane = threadIdx.x & 63;
     // BLK: code staging per wave (kDualStage steps x 64 lanes x 2 pairs)
     // (CK: the bottom row of each step, both pairs in one dword)
@@ -674,6 +674,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
     }
 }
 
+template <int MODE, bool CIGAR, bool BLK = false>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_kernel(FillArgs a) {
+    dual_fill_body<MODE, CIGAR, BLK>(a);
+}
+#if defined(TA_DUAL_BLK) && TA_DUAL_CK
+// the checkpoint fill under a name of its own (rocprof, profiles/*_by_kernel.json)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_ck_kernel(FillArgs a) {
+    dual_fill_body<TA_DUAL_MODE, true, true>(a);
+}
+#endif
+
 inline dim3 dual_grid(uint32_t waves) { return dim3((waves + kWavesPerBlock - 1) / kWavesPerBlock); }
 
 // After a pipelined dual fill: fold each couple's per-pass results in pass
@@ -727,7 +738,9 @@ template <>
 hipError_t launch_dual_mode<TA_DUAL_MODE, (TA_DUAL_CIGAR != 0)>(const FillArgs& a, hipStream_t s) {
 #endif
     if (!a.count) return hipSuccess;
-#ifdef TA_DUAL_BLK  // (its own translation unit: the blocked-layout local fill)
+#if defined(TA_DUAL_BLK) && TA_DUAL_CK  // (the checkpoint layout)
+    hipLaunchKernelGGL(dual_fill_ck_kernel, dual_grid(a.ticket ? a.n_tasks : a.count), dim3(kBlock), 0, s, a);
+#elif defined(TA_DUAL_BLK)  // (its own translation unit: the blocked-layout local fill)
     hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, true, true>), dual_grid(a.ticket ? a.n_tasks : a.count),
                        dim3(kBlock), 0, s, a);
 #else
