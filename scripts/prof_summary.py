@@ -81,7 +81,7 @@ def main():
             pmc.setdefault(k, {}).update(cs)
     with open(os.path.join(prof, f"{rtag}_pmc.json"), "w") as fh:
         json.dump(pmc, fh, indent=1)
-    fill = {k: v for k, v in pmc.items() if "fill_kernel" in k}
+    fill = {k: v for k, v in pmc.items() if "fill_kernel" in k or "fill_ck_kernel" in k}
     if fill:
         # the dominant fill launch (dual and int32 fills both match; the int32
         # one may be the near-empty fallback launch for '-' queries)
