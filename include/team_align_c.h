@@ -93,7 +93,11 @@ int ta_server_running(const ta_server* server);
  * TA_ERR_UNSERVED at once; ta_server_pause waits for the calls in flight and
  * stops the kernel, so that work on other streams of the device never queues
  * behind the persistent kernel on a shared hardware queue (a batch on the same
- * device pauses the server around its launches). */
+ * device pauses the server around its launches).  Pausing a server that is not
+ * running only counts; the drop-in shim pauses its own servers around each
+ * combined batch.  Work submitted outside the shim (ta_align_batch, plans, the
+ * mapper) does not pause anything: a caller that mixes it with a live server on
+ * one device pauses the server itself for the duration. */
 int ta_server_pause(ta_server* server);
 int ta_server_resume(ta_server* server);
 /* Diagnostics: the device-side phase times (microseconds) of the last request
