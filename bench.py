@@ -29,6 +29,10 @@ Also reported (rank 0):
                    scripts/profile.sh; rocprof counters cannot be read in-process).
   valu          -- the same kernel against the VALU int32 issue roof (the roof
                    that binds this integer DP; ops/cell from profiles/valu.json).
+  pipeline      -- the timed steps run through align.DevicePipeline (batch k's
+                   traceback beside batch k+1's fill, one workspace per slot)
+                   when two workspaces fit in HBM; the same steps one batch
+                   after the other are reported beside it (serial_*).
   host_to_host  -- the same batch through ta_align_batch from pinned host memory
                    to host results (PCIe both ways), SURVEY §8d's GCUPS definition.
   cpu_baseline  -- the reference team::Align (oracle/_ref, compiled from the
@@ -51,6 +55,13 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Hardware queues per process (HIP's default, 4, is what the box exports): the
+# pipelines (align.DevicePipeline / HostPipeline) keep fills, tracebacks,
+# uploads and downloads on streams of their own, and streams beyond the queue
+# count share queues -- two streams on one queue run one after the other.  Set
+# before anything initialises HIP.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 import numpy as np  # noqa: E402
 
@@ -98,6 +109,8 @@ def parse(argv=None):
     ap.add_argument("--gap-open", type=int, default=None,
                     help="affine-gap extension (no reference counterpart): a gap of length L costs "
                          "gap_open + L*gap, gap = the third --scoring value (config 5's 'affine gaps')")
+    ap.add_argument("--serial", action="store_true",
+                    help="one batch after the other (no DevicePipeline overlap of a traceback with the next fill)")
     ap.add_argument("--flags", type=int, default=0, help="ta_plan_create TA_PLAN_* kernel-selection flags")
     ap.add_argument("--dist-backend", default="nccl", help="nccl (= RCCL, default) or gloo (rehearsal only)")
     a = ap.parse_args(argv)
@@ -626,11 +639,23 @@ def main_align(args, D):
         cells = full.qlen.astype(np.int64) * full.tlen.astype(np.int64)
         P_max = max(h - l for l, h in shard.range_split(cells, D.world))
     gather = ResultGather(D, P_max, cigar) if D.dist else None
+    # two-slot pipeline (align.DevicePipeline): batch k's traceback beside batch k+1's fill, when
+    # a second workspace fits in HBM (config 5's 197 GB of codes does not)
+    pipe = None
+    if cigar and not args.serial:
+        free_b, _ = torch.cuda.mem_get_info(D.dev)
+        if free_b > 2 * plan.workspace_bytes + 8 * 2**30:
+            from bioinfo1_amd.align import DevicePipeline
+
+            pipe = DevicePipeline(D.dev_index, batch, mode, *sc, cigar, workspace_budget=budget,
+                                  gap_open=args.gap_open, flags=args.flags, inputs=dev_in, first=plan)
 
     def step():
-        plan.run()
+        p = pipe.step() if pipe else plan
+        if not pipe:
+            plan.run()
         if gather:
-            gather.post(plan)
+            gather.post(p)
             gather.clear_old()
 
     for _ in range(args.warmup):
@@ -666,7 +691,7 @@ def main_align(args, D):
     D.barrier()
     torch.cuda.synchronize(D.dev)
     elapsed = D.max(time.perf_counter() - t0)
-    plan.check()  # raises if a kernel reported an internal failure during the timed steps
+    (pipe or plan).check()  # raises if a kernel reported an internal failure during the timed steps
     ms = elapsed / max(args.steps, 1) * 1e3
     cells_job = (full.cells if args.workload == "cfg4" else batch.cells * D.world)
     gcups = cells_job / (ms / 1e3) / 1e9
@@ -675,6 +700,27 @@ def main_align(args, D):
     if gather and D.rank == 0:
         gathered = gather.last()
 
+    pipeline = None
+    if pipe and D.rank == 0:
+        # the same steps one batch after the other (no overlap), and the slots' results against each other
+        torch.cuda.synchronize(D.dev)
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            plan.run()
+        torch.cuda.synchronize(D.dev)
+        s_ms = (time.perf_counter() - t1) / max(args.steps, 1) * 1e3
+        same = True
+        for q in pipe.plans[1:]:
+            same = same and all(bool(torch.equal(getattr(plan, f), getattr(q, f)))
+                                for f in ("score", "target_begin", "cigar_len"))
+            if same:
+                (b0, o0), (b1, o1) = plan.compact_cigars(), q.compact_cigars()
+                same = bool(torch.equal(o0, o1)) and bool(torch.equal(b0[:int(o0[-1])], b1[:int(o1[-1])]))
+        pipeline = {"depth": len(pipe.plans), "serial_ms_per_step": round(s_ms, 4),
+                    "serial_value": round(batch.cells / (s_ms / 1e3) / 1e9, 2),
+                    "slots_bit_identical": same,
+                    "path": "align.DevicePipeline: one Aligner context (workspace) per slot; fills on a fill stream, "
+                            "tracebacks on the compute stream, batch k's traceback beside batch k+1's fill"}
     out = None
     if D.rank == 0:
         # dominant kernel (fill) timed on its own launch stream with HIP events
@@ -761,15 +807,20 @@ def main_align(args, D):
             "batch_latency_ms": round(fill_ms + (float(np.mean(tt)) if cigar else 0.0), 4),
             "chunks": plan.chunks, "workspace_gb": round(plan.workspace_bytes / 2**30, 2),
             "plan": {"dual_pairs": plan.dual_pairs, "flex_pairs": plan.flex_pairs, "fused_traceback": plan.fused},
+            "pipeline": pipeline,
             "roofline": roof, "valu": valu, "cpu_baseline": cpu, "parity": parity, **extra,
             "device": torch.cuda.get_device_name(D.dev),
         }
+    if pipe:
+        pipe.close()
     plan.close()
     al.close()
     D.close()
     if out is not None:
         print(json.dumps(out), flush=True)
         if out.get("parity") and not out["parity"].get("bit_exact", True):
+            sys.exit(1)
+        if out.get("pipeline") and not out["pipeline"]["slots_bit_identical"]:
             sys.exit(1)
         g = out.get("gather")
         if g and not g.get("bit_exact", True):
@@ -868,14 +919,14 @@ def host_to_host(runner, batch, args, reps=10):
                                      "(CIGARs compacted on the device)", "parity": par}
 
 
-def host_to_host_pipelined(al, batch, mode, sc, cigar, args, budget, reps=10):
+def host_to_host_pipelined(al, batch, mode, sc, cigar, args, budget, reps=10, overlap=True):
     """SURVEY §8d's GCUPS with the PCIe transfers overlapped (align.HostPipeline):
     every step uploads the batch from pinned host memory, runs the kernels and
     downloads every record and the compacted CIGAR bytes into pinned host memory;
     step k's upload and step k-1's download run beside the kernels."""
     from bioinfo1_amd.align import HostPipeline
 
-    hp = HostPipeline(al, batch, mode, *sc, cigar, workspace_budget=budget)
+    hp = HostPipeline(al, batch, mode, *sc, cigar, workspace_budget=budget, overlap=overlap)
     for _ in range(2):
         hp.step()
     hp.drain()

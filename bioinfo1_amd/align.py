@@ -531,6 +531,96 @@ class DevicePlan:
             pass
 
 
+class DevicePipeline:
+    """Device-resident batches aligned back to back with batch k's traceback
+    running beside batch k+1's fill.
+
+    The traceback of a batch is one long serial walk per pair -- latency-bound,
+    about one wave per SIMD -- while the fill is VALU-bound with
+    many waves per SIMD, so the two overlap well on one GPU.  Each slot is a
+    DevicePlan on its own Aligner context: the context owns the workspace the
+    fill writes and the walk reads, and ta_plan_execute_fill / _traceback order
+    one context's launches across streams (a slot's traceback waits for its
+    fill, its next fill for that traceback).  Fills run on the pipeline's fill
+    stream, tracebacks on its high-priority walk stream, and the caller's
+    current stream waits for each step's traceback, so whatever the caller
+    enqueues after step() on its stream (a compaction, a gather) follows it; a
+    slot's next fill also waits for that.  The slots share
+    one copy of the inputs.  Memory: ``depth`` workspaces."""
+
+    def __init__(self, device: int, batch, type, match, mismatch, gap, want_cigar=True, depth: int = 2,
+                 workspace_budget: int = 0, gap_open=None, flags: int = 0, inputs=None, first=None):
+        """first: an existing DevicePlan (on its own Aligner) to use as slot 0;
+        the other slots then share its inputs."""
+        import torch
+
+        self.torch = torch
+        self.dev = torch.device("cuda", device)
+        self.aligners, self.plans = [], []
+        for k in range(depth):
+            if k == 0 and first is not None:
+                self.plans.append(first)
+                continue
+            al = Aligner(device)
+            self.aligners.append(al)
+            shared = inputs if not self.plans else (self.plans[0].qbytes, self.plans[0].qoff,
+                                                    self.plans[0].tbytes, self.plans[0].toff)
+            self.plans.append(DevicePlan(al, batch, type, match, mismatch, gap, want_cigar,
+                                         workspace_budget=workspace_budget, gap_open=gap_open, flags=flags,
+                                         inputs=shared))
+        # the tracebacks on a high-priority stream: HIP gives it a hardware queue
+        # of its own (streams of one priority share GPU_MAX_HW_QUEUES queues, and
+        # the kernels of one queue run one after the other)
+        self.fill = torch.cuda.Stream(self.dev)
+        self.walk = torch.cuda.Stream(self.dev, priority=-1)
+        for st in (self.fill, self.walk):
+            st.wait_stream(torch.cuda.current_stream(self.dev))  # (the inputs' uploads)
+        self.walked = [torch.cuda.Event() for _ in range(depth)]
+        self.done = [torch.cuda.Event() for _ in range(depth)]
+        self.used = [False] * depth
+        self.k = 0
+        self.last = None
+
+    @property
+    def chunks(self):
+        return self.plans[0].chunks
+
+    def step(self):
+        """Enqueue one batch: its fill on the fill stream, its traceback on the
+        walk stream (the current stream waits for it).  Returns the slot's DevicePlan (its results are ready
+        on the current stream after the call)."""
+        torch = self.torch
+        cur = torch.cuda.current_stream(self.dev)
+        depth = len(self.plans)
+        if self.last is not None:  # the previous slot's traceback and what the caller queued after it
+            self.done[self.last].record(cur)
+        i = self.k % depth
+        self.k += 1
+        plan = self.plans[i]
+        if self.used[i]:
+            self.fill.wait_event(self.done[i])
+        for c in range(plan.chunks):
+            with torch.cuda.stream(self.fill):
+                plan.run_fill(c)
+            with torch.cuda.stream(self.walk):
+                plan.run_traceback(c)  # (waits for the fill: the slot's context orders them)
+        self.walked[i].record(self.walk)
+        cur.wait_event(self.walked[i])
+        self.used[i] = True
+        self.last = i
+        return plan
+
+    def check(self):
+        for p in self.plans:
+            p.check()
+
+    def close(self):
+        for p in self.plans:
+            p.close()
+        for al in self.aligners:
+            al.close()
+
+
 class HostBatchRunner:
     """Repeated host-memory batches (ta_align_batch) over one batch whose
     inputs and outputs live in pinned host memory (torch pin_memory, i.e.
@@ -592,16 +682,20 @@ class HostPipeline:
     CIGAR bytes back into pinned host memory (host inputs to host
     results).
 
-    Two DevicePlans alternate (double-buffered device inputs and outputs); they
-    share the aligner's context, so their kernels run one after the other.  Step
-    k enqueues its upload and kernels, then waits for step k-1's kernels (step
-    k's are already queued behind them) and downloads step k-1's records (12
-    bytes per pair) and exactly its CIGAR bytes.  Every copy is posted only
+    Two DevicePlans alternate (double-buffered device inputs and outputs), each
+    on an Aligner context of its own (the given one and a second), so that, as
+    in DevicePipeline, batch k's traceback (high-priority walk stream) runs
+    beside batch k+1's fill (fill stream).  Step k enqueues its upload and
+    kernels, then waits for step k-1's kernels and downloads step k-1's records
+    (12 bytes per pair) and exactly its CIGAR bytes.  Every copy is posted only
     once its data is ready: a copy enqueued ahead of its data (waiting on an
     event) holds its DMA engine, and an upload queued behind it then waits for
     a whole plan (measured: a 0.45 ms bubble every other step)."""
 
-    def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, workspace_budget=0):
+    def __init__(self, aligner: Aligner, batch, type, match, mismatch, gap, want_cigar=True, workspace_budget=0,
+                 overlap: bool = True):
+        """overlap=False: both slots on ``aligner``'s context, one stream for
+        the kernels (each batch's fill after the previous traceback)."""
         import torch
 
         self.torch = torch
@@ -622,11 +716,14 @@ class HostPipeline:
         self.d_t = [self.d_qt[i][nq:] for i in range(2)]
         # per slot: scores, target_begins, CIGAR lengths (written there by the plan) + the CIGAR byte total
         self.d_rec = [torch.zeros(3 * P + 1, dtype=torch.int32, device=dev) for _ in range(2)]
-        self.plans = [DevicePlan(aligner, batch, type, match, mismatch, gap, want_cigar,
+        self.second = Aligner(aligner.device) if overlap else None
+        self.plans = [DevicePlan(al, batch, type, match, mismatch, gap, want_cigar,
                                  workspace_budget=workspace_budget, inputs=(self.d_q[i], qoff, self.d_t[i], toff),
                                  records=self.d_rec[i])
-                      for i in range(2)]
-        self.compute, self.up, self.down = (torch.cuda.Stream(dev) for _ in range(3))
+                      for i, al in enumerate((aligner, self.second or aligner))]
+        self.fill, self.up, self.down = (torch.cuda.Stream(dev) for _ in range(3))
+        # tracebacks + compaction (DevicePipeline.walk); without overlap the fills run there too
+        self.compute = torch.cuda.Stream(dev, priority=-1) if overlap else self.fill
         self.h_rec = [torch.empty(3 * P + 1, dtype=torch.int32, pin_memory=True) for _ in range(2)]
         cap = max(self.plans[0].slots_bytes, 1)
         self.h_cig = [torch.empty(cap, dtype=torch.uint8, pin_memory=True) for _ in range(2)]
@@ -668,11 +765,15 @@ class HostPipeline:
             self.d_qt[i].copy_(self.h_qt, non_blocking=True)
             self.ev_in[i].record(self.up)
         plan = self.plans[i]
-        with torch.cuda.stream(self.compute):
-            self.compute.wait_event(self.ev_in[i])
+        with torch.cuda.stream(self.fill):
+            self.fill.wait_event(self.ev_in[i])
             if self.used[i]:  # the slot's results of two steps ago are down (a wait on the device)
-                self.compute.wait_event(self.ev_cig[i])
-            plan.run()
+                self.fill.wait_event(self.ev_cig[i])
+            for c in range(plan.chunks):
+                plan.run_fill(c)
+                with torch.cuda.stream(self.compute):
+                    plan.run_traceback(c)  # (after its fill: the slot's context orders them)
+        with torch.cuda.stream(self.compute):
             rec = self.d_rec[i]
             dst = None
             if self.want_cigar:
@@ -707,3 +808,5 @@ class HostPipeline:
     def close(self):
         for p in self.plans:
             p.close()
+        if self.second:
+            self.second.close()

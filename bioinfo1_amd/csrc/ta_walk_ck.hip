@@ -398,6 +398,9 @@ struct Ck2Pair {
 
 __global__ __launch_bounds__(kBlock) void traceback_ck2_kernel(TraceArgs a) {
     __shared__ Ck2Group groups[kWavesPerBlock * 4];
+    // a latency-bound chain: beside the next batch's fill (align.DevicePipeline)
+    // its instructions go first at the SIMD's issue arbiter
+    __builtin_amdgcn_s_setprio(3);
     const int lane = (int)threadIdx.x & 63, rw = lane & 15, hh = rw >> 3, lw = rw & 7;
     Ck2Group& G = groups[threadIdx.x >> 4];
     const int ma = a.match, mi = a.mismatch, gap = a.gap;

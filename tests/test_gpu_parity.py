@@ -901,6 +901,32 @@ def test_host_pipeline(aligner, oracle):
                 assert r.cigars() == want.cigars()
 
 
+def test_device_pipeline(aligner, oracle):
+    """align.DevicePipeline (batch k's traceback beside batch k+1's fill, one
+    context per slot): after several steps every slot's results equal the
+    oracle's -- checkpoint walks, the int32 path, and plans split into chunks
+    (a small workspace budget), whose fills and walks interleave per chunk."""
+    from bioinfo1_amd.align import DevicePipeline, DevicePlan
+
+    b = synth.related_batch(200, 900, 800, seed=43)
+    for mode, flags, budget in ((1, TA_PLAN_CK, 0), (1, 0, 0), (0, 0, 0), (1, TA_PLAN_CK, 12 << 20),
+                                (2, 0, 10 << 20)):
+        want = oracle.align_batch(b, mode, 1, -1, -1, True)
+        first = DevicePlan(Aligner(0), b, mode, 1, -1, -1, True, workspace_budget=budget, flags=flags)
+        pipe = DevicePipeline(0, b, mode, 1, -1, -1, True, workspace_budget=budget, flags=flags, first=first)
+        assert budget == 0 or pipe.chunks > 1
+        for _ in range(5):
+            pipe.step()
+        for plan in pipe.plans:
+            r = plan.results()
+            np.testing.assert_array_equal(r.scores, want.scores)
+            np.testing.assert_array_equal(r.target_begins, want.target_begins)
+            assert r.cigars() == want.cigars(), (mode, flags, budget)
+        pipe.close()
+        first.close()
+        first.aligner.close()
+
+
 @pytest.mark.gpu
 def test_int32_pass_pipeline(aligner, oracle):
     """Multi-pass int32 pairs run one wave per (pair, pass) (fill_pipe_kernel,
