@@ -60,8 +60,8 @@ sys.path.insert(0, ROOT)
 # uploads and downloads on streams of their own, and streams beyond the queue
 # count share queues -- two streams on one queue run one after the other.  Set
 # before anything initialises HIP.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 import numpy as np  # noqa: E402
 
