@@ -60,8 +60,9 @@ sys.path.insert(0, ROOT)
 # uploads and downloads on streams of their own, and streams beyond the queue
 # count share queues -- two streams on one queue run one after the other.  Set
 # before anything initialises HIP.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+_HWQ = int(os.environ.get("TA_BENCH_HW_QUEUES", "16"))  # (experiments: another count)
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _HWQ or "TA_BENCH_HW_QUEUES" in os.environ:
+    os.environ["GPU_MAX_HW_QUEUES"] = str(min(_HWQ, 32))
 
 import numpy as np  # noqa: E402
 
@@ -80,7 +81,7 @@ DTYPE = "int32 semantics; packed int16 arithmetic where range-proven (fits_int16
 def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="cfg2", choices=["cfg2", "cfg3", "cfg4", "cfg5", "cfg3map", "dropin"],
                     help="cfg2: 1kx1k pairs (headline); cfg3: E. coli stand-in, ONT-like reads vs true-origin "
