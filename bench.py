@@ -61,6 +61,8 @@ sys.path.insert(0, ROOT)
 # count share queues -- two streams on one queue run one after the other.  Set
 # before anything initialises HIP.
 _HWQ = int(os.environ.get("TA_BENCH_HW_QUEUES", "16"))  # (experiments: another count)
+_HWQ_ORIG = os.environ.get("GPU_MAX_HW_QUEUES")  # (the drop-in runs keep the process default: more
+# queues cost the single-pair server's 5x9 round trip 13 -> 19 us)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _HWQ or "TA_BENCH_HW_QUEUES" in os.environ:
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(_HWQ, 32))
 
@@ -966,6 +968,14 @@ def workload_name(args, cigar, n_pairs, full):
                   f"{tail}")
 
 
+def _dropin_env(extra):
+    e = dict(os.environ, **extra)
+    e.pop("GPU_MAX_HW_QUEUES", None)
+    if _HWQ_ORIG is not None:
+        e["GPU_MAX_HW_QUEUES"] = _HWQ_ORIG
+    return e
+
+
 def main_dropin(args):
     """Single-call team::Align (the reference mapper's calling pattern) through
     our drop-in library vs the reference's own Align, same harness, same pairs."""
@@ -980,7 +990,7 @@ def main_dropin(args):
         rows = []
         for thr in (1, 8, 16):  # 16: the host cores a GPU box grants this job
             p = subprocess.run([exe, str(thr), "1.0", "5x9,200x200,1000x1000", str(MODES[args.mode or "local"])],
-                               capture_output=True, text=True, timeout=300, check=True, env=dict(os.environ, **env))
+                               capture_output=True, text=True, timeout=300, check=True, env=_dropin_env(env))
             rows += [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
         res[name] = rows
     same = None
