@@ -11,7 +11,9 @@ OUT="$ROOT/gpurun_out/$TAG"
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-BARGS=(--steps 3 --warmup 1 --no-cpu --no-parity --no-host --no-score-only "$@")
+# --serial: one batch after the other, so that no two kernels' durations and
+# counters overlap (the pipelined steps run a walk beside the next fill)
+BARGS=(--steps 20 --warmup 3 --serial --no-cpu --no-parity --no-host --no-score-only "$@")
 step() { # name timeout args...
   local name=$1 to=$2; shift 2
   echo "== $name" | tee -a "$OUT/profile.log"
