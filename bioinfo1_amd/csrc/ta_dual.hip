@@ -681,6 +681,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
 #if defined(TA_DUAL_BLK) && TA_DUAL_CK
 // the checkpoint fill under a name of its own (rocprof, profiles/*_by_kernel.json)
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_ck_kernel(FillArgs a) {
+#ifdef TA_FILL_PRIO
+    __builtin_amdgcn_s_setprio(TA_FILL_PRIO);
+#endif
     dual_fill_body<TA_DUAL_MODE, true, true>(a);
 }
 #endif

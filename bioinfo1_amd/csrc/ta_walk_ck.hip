@@ -400,7 +400,10 @@ __global__ __launch_bounds__(kBlock) void traceback_ck2_kernel(TraceArgs a) {
     __shared__ Ck2Group groups[kWavesPerBlock * 4];
     // a latency-bound chain: beside the next batch's fill (align.DevicePipeline)
     // its instructions go first at the SIMD's issue arbiter
-    __builtin_amdgcn_s_setprio(3);
+#ifndef TA_WALK_PRIO
+#define TA_WALK_PRIO 3
+#endif
+    __builtin_amdgcn_s_setprio(TA_WALK_PRIO);
     const int lane = (int)threadIdx.x & 63, rw = lane & 15, hh = rw >> 3, lw = rw & 7;
     Ck2Group& G = groups[threadIdx.x >> 4];
     const int ma = a.match, mi = a.mismatch, gap = a.gap;

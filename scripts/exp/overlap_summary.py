@@ -20,5 +20,16 @@ out = {"trace": sys.argv[1], "fills": len(fills), "walks": len(walks),
        "walks_mostly_overlapped": sum(x > 0.5 for x in ov),
        "mean_fill_us": round(sum(e - s for s, e in fills) / max(len(fills), 1) / 1e3, 1),
        "mean_walk_us": round(sum(e - s for s, e in walks) / max(len(walks), 1) / 1e3, 1)}
+pw = [(s, e) for (s, e), x in zip(walks, ov) if x > 0.5]
+pf = [(fs, fe) for fs, fe in fills if any(min(fe, e) > max(fs, s) for s, e in walks)]
+out["pipelined_walk_us"] = round(sum(e - s for s, e in pw) / max(len(pw), 1) / 1e3, 1)
+out["pipelined_fill_us"] = round(sum(e - s for s, e in pf) / max(len(pf), 1) / 1e3, 1)
+if pf:  # fill starts of the overlapped stretch: the per-batch period
+    st = sorted(s for s, e in pf)
+    out["pipelined_fill_period_us"] = round((st[-1] - st[0]) / max(len(st) - 1, 1) / 1e3, 1)
+sw = [(s, e) for (s, e), x in zip(walks, ov) if x == 0.0]
+sf = [(fs, fe) for fs, fe in fills if (fs, fe) not in pf]
+out["serial_walk_us"] = round(sum(e - s for s, e in sw) / max(len(sw), 1) / 1e3, 1)
+out["serial_fill_us"] = round(sum(e - s for s, e in sf) / max(len(sf), 1) / 1e3, 1)
 json.dump(out, open(sys.argv[2], "w"), indent=1)
 print(json.dumps(out)[:600])
