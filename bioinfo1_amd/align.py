@@ -436,6 +436,18 @@ class DevicePlan:
     def _stream(self):
         return C.c_void_p(self.torch.cuda.current_stream(self.dev).cuda_stream)
 
+    def set_inputs(self, inputs):
+        """Point the plan at another batch of the same shapes already in HBM:
+        (query bytes, query offsets, target bytes, target offsets) tensors --
+        pair p must keep its planned lengths.  Takes effect for the launches
+        enqueued after the call; the caller keeps the tensors unmodified until
+        those launches are done."""
+        q, qo, t, to = inputs
+        assert q.device == self.dev and t.device == self.dev and qo.numel() >= self.P and to.numel() >= self.P
+        self.qbytes, self.qoff, self.tbytes, self.toff = q, qo, t, to
+        self.io.query_bytes, self.io.query_off = q.data_ptr(), qo.data_ptr()
+        self.io.target_bytes, self.io.target_off = t.data_ptr(), to.data_ptr()
+
     def run(self):
         r = self._fn("ta_plan_execute")(self._h, C.byref(self.io), self._stream())
         if r != TA_OK:
@@ -544,14 +556,23 @@ class DevicePipeline:
     fill, its next fill for that traceback).  Fills run on the pipeline's fill
     stream, tracebacks on its high-priority walk stream, and the caller's
     current stream waits for each step's traceback, so whatever the caller
-    enqueues after step() on its stream (a compaction, a gather) follows it; a
-    slot's next fill also waits for that.  The slots share
-    one copy of the inputs.  Memory: ``depth`` workspaces."""
+    enqueues after step() on its stream (a compaction, a gather, the next
+    upload into this step's input buffers) follows it; a slot's next fill also
+    waits for that.
+
+    Inputs: every step may align another batch of the planned shapes
+    (step(inputs=...), tensors in HBM); the step's fill waits for the
+    ``ready`` event (recorded after the batch's upload, e.g. on a copy stream).
+    Without ``ready`` the inputs must already be resident (written before the
+    pipeline was built, or synchronised): waiting on the caller's stream would
+    also wait for the previous step's traceback and serialise the pipeline.  A
+    step without inputs realigns the slot's last batch (at construction: the
+    shared first batch).  Memory: ``depth`` workspaces."""
 
     def __init__(self, device: int, batch, type, match, mismatch, gap, want_cigar=True, depth: int = 2,
                  workspace_budget: int = 0, gap_open=None, flags: int = 0, inputs=None, first=None):
         """first: an existing DevicePlan (on its own Aligner) to use as slot 0;
-        the other slots then share its inputs."""
+        the other slots then start on its inputs."""
         import torch
 
         self.torch = torch
@@ -585,10 +606,14 @@ class DevicePipeline:
     def chunks(self):
         return self.plans[0].chunks
 
-    def step(self):
+    def step(self, inputs=None, ready=None):
         """Enqueue one batch: its fill on the fill stream, its traceback on the
-        walk stream (the current stream waits for it).  Returns the slot's DevicePlan (its results are ready
-        on the current stream after the call)."""
+        walk stream (the current stream waits for it).  inputs: this batch's
+        (query bytes, query offsets, target bytes, target offsets) tensors in
+        HBM, same shapes as planned; ready: an event the fill waits for first
+        (None: the inputs are resident).  Returns the slot's
+        DevicePlan (its results are ready on the current stream after the call;
+        the inputs may be overwritten by work enqueued on it after the call)."""
         torch = self.torch
         cur = torch.cuda.current_stream(self.dev)
         depth = len(self.plans)
@@ -599,6 +624,10 @@ class DevicePipeline:
         plan = self.plans[i]
         if self.used[i]:
             self.fill.wait_event(self.done[i])
+        if inputs is not None:
+            plan.set_inputs(inputs)
+            if ready is not None:
+                self.fill.wait_event(ready)
         for c in range(plan.chunks):
             with torch.cuda.stream(self.fill):
                 plan.run_fill(c)

@@ -139,6 +139,13 @@ __device__ __forceinline__ uint32_t bfi(uint32_t mask, uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t swar_k(int v) { return (uint32_t)(v * 65537); }
 __device__ __forceinline__ uint32_t swar_add(uint32_t a, uint32_t k) { return a + k; }
 
+// each half shifted right by 4 (v_pk_lshrrev_b16)
+__device__ __forceinline__ uint32_t pk_lshr4(uint32_t a) {
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u2, a) >> (u2){4, 4});
+}
+// (a & m) | (b & ~m) with a per-lane mask (bfi above takes a wave-uniform one)
+__device__ __forceinline__ uint32_t vsel(uint32_t m, uint32_t a, uint32_t b) { return (a & m) | (b & ~m); }
+
 // 0xFFFF in each half whose sign bit (15 / 31) is set
 __device__ __forceinline__ uint32_t half_mask(uint32_t x) { return __builtin_amdgcn_perm(x, x, 0x09090808u); }
 __device__ __forceinline__ uint32_t rep16(int v) { return ((uint32_t)v & 0xFFFFu) | ((uint32_t)v << 16); }

@@ -123,3 +123,131 @@ def test_window_walk_matches_reference(sc):
         if H[gi, gj] <= 0:
             continue
         assert window_walk(H, D, I, gi, gj, q, t, sc) == reference_walk(H, D, I, gi, gj), (sc, k)
+
+
+def ck_row_index(pss, t, lane, nb):  # ta_layout.h
+    return (pss * nb * 2 * 64 + (t >> 4) * 64 + lane) * 16 + (t & 15)
+
+
+def ck_col_index(pss, b, lane, nb, r):
+    return ((pss * 2 + 1) * nb * 64 + b * 64 + lane) * 16 + r
+
+
+@pytest.mark.parametrize("n,m", [(1000, 1000), (1030, 990), (2100, 700), (40, 1200), (1500, 64), (300, 280),
+                                 (1, 1), (17, 33), (1100, 1100)])
+def test_window_loads_in_bounds(n, m):
+    """Every HBM load of the walk kernel's window (traceback_ck_kernel, its
+    index arithmetic restated for every cell (i, j) a walk can stand on and
+    every lane of a group) lies inside the pair's checkpoint region, target and
+    query, and the top-row loads of columns > 0 address ck_row_index of the
+    stripe above exactly (block offsets of +1024 / +2048 from two bases)."""
+    nb = (m + 63 + 15) // 16
+    region = ((n + 1023) // 1024) * nb * 2048  # int16 entries (ptr_dwords_blk * 2)
+    j = np.arange(1, m + 1, dtype=np.int64)
+    for i in range(1, n + 1):
+        g = (i - 1) >> 4
+        l = g & 63
+        e = j - LEAD + l
+        c0 = np.where(e >= 16, np.maximum((e >> 4) * 16 - l, 0), 0)
+        W = j - c0
+        assert (W >= 1).all() and (W <= LEAD + 15).all()
+        for lg in range(8):
+            li = np.where(c0 > 0, ck_col_index(g >> 6, (e >> 4) - 1, l, nb, 2 * lg), 0)
+            assert (li >= 0).all() and (li + 1 < region).all()
+            if g > 0:
+                gu = g - 1
+                lu, pu = gu & 63, gu >> 6
+                t0 = c0 + lg + lu - 1
+                t1 = t0 + 8
+                base = pu * nb * 2048 + lu * 16
+                i0 = base + (t0 >> 4) * 1024 + (t0 & 15)
+                i1 = base + (t1 >> 4) * 1024 + (t1 & 15)
+                for q, idx in enumerate((np.maximum(i0, 0), i1, i0 + 1024, i1 + 1024, i0 + 2048)):
+                    assert (idx >= 0).all() and (idx < region).all(), (n, m, i, lg, q)
+                    col = c0 + lg + 8 * q
+                    ok = col > 0
+                    assert (idx[ok] == ck_row_index(pu, col[ok] + lu - 1, lu, nb)).all(), (n, m, i, lg, q)
+            for q in range(4):
+                x = 1 + lg + 8 * q
+                tix = (c0 + x - 1)[x <= W]
+                assert (tix >= 0).all() and (tix < m).all()
+            assert 0 <= min(16 * g + 2 * lg + 1, n - 1) < n
+
+
+def kernel_events_walk(H, D, I, i, j):
+    """The kernel's walk at the bit level (traceback_ck_kernel): per window the
+    row words NI = ~I | D, D and H = 0 of W bits (column x at bit W - x), the
+    row steps with the 33-bit run bound, records, and the events of the records
+    with the I run carried across windows -- expanded into ops (walk order)."""
+    ev, kI = [], 0
+    while True:
+        g, r = (i - 1) >> 4, (i - 1) & 15
+        lane = g & 63
+        e = j - LEAD + lane
+        c0 = max((e >> 4) * 16 - lane, 0) if e >= 16 else 0
+        W = j - c0
+        rows = {}
+        for rr in range(r + 1):
+            a = 16 * g + rr + 1
+            iw = dw = zw = 0
+            for x in range(1, W + 1):
+                b, bit = c0 + x, 1 << (W - x)
+                iw |= bit if I[a, b] else 0
+                dw |= bit if D[a, b] else 0
+                zw |= bit if H[a, b] == 0 else 0
+            rows[rr] = ((~iw | dw) & 0xFFFFFFFF, dw, zw)
+        pos, rr, wl, zdone, recs = 0, r, 1, 0, []
+        while wl:
+            ni, dw, zw = rows[rr]
+            zero = (zw >> pos) & 1
+            v = (ni >> pos) | (1 << 32)
+            run = min((v & -v).bit_length() - 1, W - pos)
+            p1 = pos + run
+            edge = 1 if p1 >= W else 0
+            dmove = (dw >> (p1 & 31)) & 1
+            go = wl & (zero ^ 1)
+            mv = go & (edge ^ 1)
+            if go:
+                recs.append(run | (dmove << 8) | (edge << 9))
+            pos += go * run + (mv & (dmove ^ 1))
+            rr -= mv
+            zdone |= wl & zero
+            wl = mv & (1 if rr >= 0 else 0) & (1 if pos < W else 0)
+        for k, rc in enumerate(recs):
+            runI = (rc & 63) + (kI if k == 0 else 0)
+            if rc & 0x200:
+                continue
+            if runI:
+                ev.append((runI << 2) | 1)
+            ev.append(((1 << 16) | 3) if rc & 0x100 else 4)
+        if recs:
+            last = recs[-1]
+            kI = ((last & 63) + (kI if len(recs) == 1 else 0)) if last & 0x200 else 0
+        i, j = 16 * g + rr + 1, c0 + W - pos
+        if zdone or i < 1 or j < 1:
+            break
+    ops = []
+    for v in ev:
+        kd, bc, mop = v >> 16, (v >> 2) & 0x3FFF, v & 3
+        ops += ["D"] * kd
+        if mop != 3:
+            ops += ["MID"[mop]] * bc
+    return "".join(reversed(ops))
+
+
+@pytest.mark.parametrize("sc", [(1, -1, -1), (2, -3, -1), (3, 4, 0)])
+def test_kernel_events_walk_matches_reference(sc):
+    """The bit-level walk and its events give the reference path, including I
+    runs that cross several 32-column windows (the run bound of a full window)."""
+    rng = np.random.default_rng(0xE7 + sc[0])
+    al = b"ACGT"
+    for k, (n, m, ins) in enumerate([(120, 200, 70), (90, 160, 45), (70, 90, 0), (200, 150, 33), (60, 140, 64)]):
+        q = bytes(al[v] for v in rng.integers(4, size=n))
+        t = bytes(al[v] for v in rng.integers(4, size=m))
+        if ins:
+            cut = n // 2
+            t = (q[:cut] + b"N" * ins + q[cut:] + t)[:m]
+        H, D, I, gi, gj = dp(q, t, *sc)
+        if H[gi, gj] <= 0:
+            continue
+        assert kernel_events_walk(H, D, I, gi, gj) == reference_walk(H, D, I, gi, gj), (sc, k)

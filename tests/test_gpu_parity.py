@@ -903,25 +903,41 @@ def test_host_pipeline(aligner, oracle):
 
 def test_device_pipeline(aligner, oracle):
     """align.DevicePipeline (batch k's traceback beside batch k+1's fill, one
-    context per slot): after several steps every slot's results equal the
-    oracle's -- checkpoint walks, the int32 path, and plans split into chunks
-    (a small workspace budget), whose fills and walks interleave per chunk."""
+    context per slot) over THREE different batches of one shape in turn, so each
+    slot gets a different batch at every use (depth 2): every step's results --
+    snapshotted on the caller's stream right after the step, with no sync in
+    between -- equal the oracle's for its own batch.  A walk reading a workspace
+    its slot's next fill already overwrote, or a fill starting before its own
+    batch's inputs, shows up as another batch's results.  Checkpoint walks, the
+    int32 path, and plans split into chunks (a small workspace budget), whose
+    fills and walks interleave per chunk."""
+    import torch
+
     from bioinfo1_amd.align import DevicePipeline, DevicePlan
 
-    b = synth.related_batch(200, 900, 800, seed=43)
+    bs = [synth.related_batch(200, 900, 800, seed=43 + v) for v in range(3)]
+    dev = torch.device("cuda", 0)
+    ins = [tuple(torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+                 for a in (b.qbytes, b.qoff.view(np.int64), b.tbytes, b.toff.view(np.int64))) for b in bs]
+    torch.cuda.synchronize()
     for mode, flags, budget in ((1, TA_PLAN_CK, 0), (1, 0, 0), (0, 0, 0), (1, TA_PLAN_CK, 12 << 20),
                                 (2, 0, 10 << 20)):
-        want = oracle.align_batch(b, mode, 1, -1, -1, True)
-        first = DevicePlan(Aligner(0), b, mode, 1, -1, -1, True, workspace_budget=budget, flags=flags)
-        pipe = DevicePipeline(0, b, mode, 1, -1, -1, True, workspace_budget=budget, flags=flags, first=first)
+        wants = [oracle.align_batch(b, mode, 1, -1, -1, True) for b in bs]
+        first = DevicePlan(Aligner(0), bs[0], mode, 1, -1, -1, True, workspace_budget=budget, flags=flags)
+        pipe = DevicePipeline(0, bs[0], mode, 1, -1, -1, True, workspace_budget=budget, flags=flags, first=first)
         assert budget == 0 or pipe.chunks > 1
-        for _ in range(5):
-            pipe.step()
-        for plan in pipe.plans:
-            r = plan.results()
-            np.testing.assert_array_equal(r.scores, want.scores)
-            np.testing.assert_array_equal(r.target_begins, want.target_begins)
-            assert r.cigars() == want.cigars(), (mode, flags, budget)
+        snaps = []
+        for k in range(7):
+            plan = pipe.step(inputs=ins[k % 3])
+            dst, off = plan.compact_cigars()
+            snaps.append((k % 3, plan.score.clone(), plan.target_begin.clone(), plan.cigar_len.clone(), dst, off))
+        pipe.check()
+        for v, sc, tb, cl, dst, off in snaps:
+            want = wants[v]
+            np.testing.assert_array_equal(sc.cpu().numpy(), want.scores)
+            np.testing.assert_array_equal(tb.cpu().numpy().view(np.uint32), want.target_begins)
+            np.testing.assert_array_equal(cl.cpu().numpy().view(np.uint32), want.cigar_lens)
+            assert dst[:int(off[-1])].cpu().numpy().tobytes() == b"".join(want.cigars()), (mode, flags, budget, v)
         pipe.close()
         first.close()
         first.aligner.close()
