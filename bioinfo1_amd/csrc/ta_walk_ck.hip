@@ -61,13 +61,31 @@ static_assert(8 * kCkBlocks <= 40, "a row's steps fit 40 bits (one byte + one dw
 
 struct CkGroup {
     uint32_t top[8 * kCkBlocks + 1];     // per x: both pairs' H(16g, c0 + x) + gap + B (int16 halves)
-    uint32_t tb[8 + 8 * kCkBlocks + 1];  // per x (at 8 + x): both pairs' target bytes (bits 7:0, 23:16)
+    // per x (at 8 + x): both pairs' gain tables of the target byte (TAB windows: .x pair
+    // A's, .y pair B's, ckGainTable), else their target bytes (.x bits 7:0, 23:16)
+    uint2 tb[8 + 8 * kCkBlocks + 1];
     // (after top / tb: the walk reads the row above row 0 -- up to 18 rows -- of
     // walkers that already left, from inside the group)
     uint4 row[2][16];                    // per pair and row: NI, D, H = 0 window words
     uint32_t rec[2][16];                 // per pair: the window's row steps
 };
 static_assert(offsetof(CkGroup, row) >= 18 * sizeof(uint4), "room above a walker's row 0");
+
+// TAB windows (every query row of both pairs is A, C, G or T; ta_packed.h
+// mismatch_table): the diagonal gain of a cell is a byte of its column's gain
+// table -- byte k = (s - gap) + 128 for the query letter of class k, s = match
+// when the target byte is that letter, else mismatch -- picked for both pairs by
+// one v_perm with the row's selector (row_selector: pair A's byte in bits 7:0,
+// B's in 23:16) and added as ONE 32-bit add3 with -128 * 65537.  Exact when both
+// halves of the sum lie in [0, 2^16): true of every value the window holds for a
+// column x <= W of its pair, and kept true past W by masking the top row and the
+// rows past n to H = 0 (a borrow from pair A's half would change pair B's cell).
+__device__ __forceinline__ uint32_t ck_gain_table(uint32_t c, int ua, int ub) {
+    const uint32_t k = (c >> 1) & 3u;
+    const bool hit = c == ((0x47544341u >> (8u * k)) & 0xFFu);  // 'A', 'C', 'T', 'G'
+    const uint32_t t = (uint32_t)ub * 0x01010101u;
+    return hit ? (t & ~(0xFFu << (8u * k))) | ((uint32_t)ua << (8u * k)) : t;
+}
 
 __device__ __forceinline__ void ck_wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
@@ -108,8 +126,11 @@ struct CkPair {
     bool has;
 };
 
-__global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
+// (<= 128 VGPRs: beside the next batch's fill -- 96 VGPRs a wave -- a walk wave then displaces
+// one fill wave of its SIMD, not two)
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void traceback_ck_kernel(TraceArgs a) {
     __shared__ CkGroup groups[kWavesPerBlock * kCkGroups];
+    __shared__ uint32_t gtab[256];  // ck_gain_table of every byte value
     // a latency-bound chain: beside the next batch's fill (align.DevicePipeline)
     // its instructions go first at the SIMD's issue arbiter (measured neutral)
     __builtin_amdgcn_s_setprio(3);
@@ -164,6 +185,14 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // (see ta_packed.h pk_min_u16)
     const bool first = lg == 0;
+    // TAB windows need both gains (s - gap) in [-128, 127]
+    const int ua = ma - gap + 128, ub = mi - gap + 128;
+    const bool tab_ok = (uint32_t)ua < 256u && (uint32_t)ub < 256u;
+    gtab[threadIdx.x] = ck_gain_table(threadIdx.x, ua, ub);  // (kBlock == 256: one byte value per thread)
+    static_assert(kBlock == 256, "one gain table entry per thread");
+    __syncthreads();
+    uint32_t KN = swar_k(-128);
+    asm volatile("" : "+s"(KN));
     uint32_t acc[3][kCkBlocks];
 #pragma unroll
     for (int b = 0; b < kCkBlocks; ++b) acc[0][b] = acc[1][b] = acc[2][b] = 0u;
@@ -208,45 +237,64 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
                 const int x = 1 + lg + 8 * q;
                 vb[h][q] = x <= W[h] ? (uint32_t)c.T[c0[h] + x - 1] : 0u;
             }
-            // query bytes of the lane's rows (rows past n: any byte, below the walk)
+            // query bytes of the lane's rows (rows past n: any byte, below the walk; pairs
+            // not walking: 'A', which keeps a TAB window)
             const uint32_t ir = 16u * (uint32_t)g[h] + 2u * (uint32_t)lg;  // the first row - 1
             const uint32_t qn = c.n ? c.n - 1u : 0u;
-            vq[h][0] = c.Q[min(ir, qn)];
-            vq[h][1] = c.Q[min(ir + 1u, qn)];
+            vq[h][0] = live[h] ? c.Q[min(ir, qn)] : 0x41u;
+            vq[h][1] = live[h] ? c.Q[min(ir + 1u, qn)] : 0x41u;
         }
         // decodes (ta_layout.h ck_decode, plus gap + B): v = (s - off - zstep j + i - dl l) / 16 + gap + B
         // is exact in 16-bit wrap-around arithmetic ((s + C) mod 2^16 = 16 (H + gap + B) < 2^16),
         // so both pairs decode together: one packed add of C and one packed shift
-        uint32_t gl0, gl1, q0, q1, mT = 0, mL = 0;
+        uint32_t gl0, gl1, q0, q1, mT = 0, mL0 = 0, mL1 = 0;
+        bool acgt = true;
         {
             int CL[2], CT[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const CkPair& c = S[h];
                 const int l = g[h] & 63, lu = (g[h] - 1) & 63;
-                CL[h] = 16 * GB - c.off - zstep * c0[h] + (16 * g[h] + 2 * lg + 1) - c.dl * l;
+                const int ir = 16 * g[h] + 2 * lg + 1;  // the lane's first row
+                CL[h] = 16 * GB - c.off - zstep * c0[h] + ir - c.dl * l;
                 CT[h] = 16 * GB - c.off - zstep * (c0[h] + lg) + 16 * g[h] - c.dl * lu;
-                mL |= (live[h] && c0[h] > 0) ? 0xFFFFu << (16 * h) : 0u;
+                // (rows past n: H = 0 too, see ck_gain_table)
+                const bool hl = live[h] && c0[h] > 0;
+                mL0 |= (hl && ir <= (int)c.n) ? 0xFFFFu << (16 * h) : 0u;
+                mL1 |= (hl && ir + 1 <= (int)c.n) ? 0xFFFFu << (16 * h) : 0u;
                 mT |= (live[h] && g[h] > 0) ? 0xFFFFu << (16 * h) : 0u;
+                acgt = acgt && is_acgt(vq[h][0]) && is_acgt(vq[h][1]);
             }
             const uint32_t cl = ((uint32_t)CL[0] & 0xFFFFu) | ((uint32_t)CL[1] << 16);
             const uint32_t ct = ((uint32_t)CT[0] & 0xFFFFu) | ((uint32_t)CT[1] << 16);
             const uint32_t l0 = __builtin_amdgcn_perm(vl[1], vl[0], 0x05040100u);  // row 2 lg of A, B
             const uint32_t l1 = __builtin_amdgcn_perm(vl[1], vl[0], 0x07060302u);  // row 2 lg + 1
-            gl0 = vsel(mL, pk_lshr4(pk_add(l0, cl)), GB2);
-            gl1 = vsel(mL, pk_lshr4(pk_add(l1, pk_add(cl, ONE))), GB2);
+            gl0 = vsel(mL0, pk_lshr4(pk_add(l0, cl)), GB2);
+            gl1 = vsel(mL1, pk_lshr4(pk_add(l1, pk_add(cl, ONE))), GB2);
             // column 0 (c0 = 0, x = 0): H = 0
             const uint32_t m0 = mT & (lg == 0 ? ((c0[0] > 0 ? 0xFFFFu : 0u) | (c0[1] > 0 ? 0xFFFF0000u : 0u)) : ~0u);
             const uint32_t dx = rep16(-8 * zstep);  // the decode constant moves by -zstep per column
             uint32_t ctq = ct;
 #pragma unroll
             for (int q = 0; q < 5; ++q) {
+                // (columns past W: H = 0, see ck_gain_table)
+                const int x = lg + 8 * q;
+                const uint32_t mw = (x <= W[0] ? 0xFFFFu : 0u) | (x <= W[1] ? 0xFFFF0000u : 0u);
                 const uint32_t s = vt[0][q] | (vt[1][q] << 16);
-                G.top[lg + 8 * q] = vsel(q == 0 ? m0 : mT, pk_lshr4(pk_add(s, ctq)), GB2);
+                G.top[x] = vsel((q == 0 ? m0 : mT) & mw, pk_lshr4(pk_add(s, ctq)), GB2);
                 ctq = pk_add(ctq, dx);
             }
+        }
+        // the window's sweep kind (wave-uniform): TAB when every query row is A, C, G, T
+        const bool tab = tab_ok && !ballot(!acgt);
+        if (tab) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) G.tb[9 + lg + 8 * q] = vb[0][q] | (vb[1][q] << 16);
+            for (int q = 0; q < 4; ++q) G.tb[9 + lg + 8 * q] = make_uint2(gtab[vb[0][q]], gtab[vb[1][q]]);
+            q0 = row_selector(vq[0][0], vq[1][0]);
+            q1 = row_selector(vq[0][1], vq[1][1]);
+        } else {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) G.tb[9 + lg + 8 * q] = make_uint2(vb[0][q] | (vb[1][q] << 16), 0u);
             q0 = vq[0][0] | (vq[1][0] << 16);
             q1 = vq[0][1] | (vq[1][1] << 16);
         }
@@ -255,14 +303,17 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
         // ---- the sweep: step k, lane lg computes column x = k - lg + 1 of its two rows of both pairs
         const int need = max(W[0], W[1]) + kCkLanes - 1;  // steps this lane's pairs need
         uint32_t upp = G.top[0];  // the previous step's up candidate of row 2 lg (lane 0: H(16g, c0) + gap + B)
-        const uint32_t* tbl = &G.tb[9 - lg];
-        auto block = [&](auto kb_tag) {
+        const uint2* tbl = &G.tb[9 - lg];
+        auto block = [&](auto kb_tag, auto tab_tag) {
             constexpr int kb = decltype(kb_tag)::value;
-            uint32_t tv[8], bv[8];
+            constexpr bool TAB = decltype(tab_tag)::value;
+            uint32_t tv[8];
+            uint2 bv[8];
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 tv[s] = G.top[kb + s + 1];
-                bv[s] = tbl[kb + s];
+                if constexpr (TAB) bv[s] = tbl[kb + s];
+                else bv[s].x = tbl[kb + s].x;
             }
             uint32_t a0 = acc[0][kb / 8], a1 = acc[1][kb / 8], a2 = acc[2][kb / 8];
 #pragma unroll
@@ -271,12 +322,15 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
                 // group's first lane: the top row), diagonal = the previous step's up
                 const uint32_t dpp = (uint32_t)__builtin_amdgcn_mov_dpp((int)gl1, 0x111, 0xF, 0xF, true);
                 const uint32_t up0 = first ? tv[s] : dpp;
-                const uint32_t dg0 = pk_mad_i16(pk_min_u16(q0 ^ bv[s], ONE), KD2, pk_add(upp, SA2));
+                uint32_t dg0, dg1;
+                if constexpr (TAB) dg0 = upp + mismatch_flags(bv[s].x, bv[s].y, q0) + KN;  // (v_add3_u32)
+                else dg0 = pk_mad_i16(pk_min_u16(q0 ^ bv[s].x, ONE), KD2, pk_add(upp, SA2));
                 const uint32_t m10 = pk_max(dg0, gl0);
                 const uint32_t hn0 = pk_max3_pos(m10, up0, B2);  // H + B (clamp at H = 0)
                 const uint32_t gn0 = pk_add(hn0, GAP2);
                 // the second row: up = the first row's new value, diagonal = its previous one
-                const uint32_t dg1 = pk_mad_i16(pk_min_u16(q1 ^ bv[s], ONE), KD2, pk_add(gl0, SA2));
+                if constexpr (TAB) dg1 = gl0 + mismatch_flags(bv[s].x, bv[s].y, q1) + KN;
+                else dg1 = pk_mad_i16(pk_min_u16(q1 ^ bv[s].x, ONE), KD2, pk_add(gl0, SA2));
                 const uint32_t m11 = pk_max(dg1, gl1);
                 const uint32_t hn1 = pk_max3_pos(m11, gn0, B2);
                 const uint32_t gn1 = pk_add(hn1, GAP2);
@@ -295,15 +349,19 @@ __global__ __launch_bounds__(kBlock) void traceback_ck_kernel(TraceArgs a) {
             acc[1][kb / 8] = a1;
             acc[2][kb / 8] = a2;
         };
-        block(std::integral_constant<int, 0>{});
-        block(std::integral_constant<int, 8>{});
-        if (ballot(need > 16)) {
-            block(std::integral_constant<int, 16>{});
-            if (ballot(need > 24)) {
-                block(std::integral_constant<int, 24>{});
-                if (ballot(need > 32)) block(std::integral_constant<int, 32>{});
+        auto sweep = [&](auto tab_tag) {
+            block(std::integral_constant<int, 0>{}, tab_tag);
+            block(std::integral_constant<int, 8>{}, tab_tag);
+            if (ballot(need > 16)) {
+                block(std::integral_constant<int, 16>{}, tab_tag);
+                if (ballot(need > 24)) {
+                    block(std::integral_constant<int, 24>{}, tab_tag);
+                    if (ballot(need > 32)) block(std::integral_constant<int, 32>{}, tab_tag);
+                }
             }
-        }
+        };
+        if (tab) sweep(std::true_type{});
+        else sweep(std::false_type{});
         // Per pair and row: step k at bit 39 - k of a 40-bit row (block b's byte at bits
         // 8 (4 - b)); column x = k - lg + 1 at bit W - x of the window word: bits
         // [8 - lg, 40 - lg) of the row, shifted down by 32 - W.  (Steps past the blocks

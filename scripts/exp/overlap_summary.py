@@ -7,7 +7,7 @@ import sys
 rows = list(csv.DictReader(open(sys.argv[1])))
 k = [(int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"], r["Queue_Id"]) for r in rows]
 fills = [(s, e) for s, e, n, q in k if "dual_fill_ck_kernel" in n]
-walks = [(s, e) for s, e, n, q in k if "traceback_ck2_kernel" in n]
+walks = [(s, e) for s, e, n, q in k if "traceback_ck_kernel" in n]
 ov = []
 for s, e in walks:
     t = sum(max(0, min(e, fe) - max(s, fs)) for fs, fe in fills)
@@ -15,7 +15,7 @@ for s, e in walks:
 span = max(e for s, e, n, q in k if "ta::" in n) - min(s for s, e, n, q in k if "ta::" in n)
 out = {"trace": sys.argv[1], "fills": len(fills), "walks": len(walks),
        "fill_queues": sorted({q for s, e, n, q in k if "dual_fill_ck_kernel" in n}),
-       "walk_queues": sorted({q for s, e, n, q in k if "traceback_ck2_kernel" in n}),
+       "walk_queues": sorted({q for s, e, n, q in k if "traceback_ck_kernel" in n}),
        "walk_share_overlapping_a_fill": [round(x, 3) for x in ov],
        "walks_mostly_overlapped": sum(x > 0.5 for x in ov),
        "mean_fill_us": round(sum(e - s for s, e in fills) / max(len(fills), 1) / 1e3, 1),
