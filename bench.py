@@ -626,12 +626,52 @@ def dominant_kernel(plan, mode, cigar, affine):
     return f"fill_kernel<{mode}, {c}, false>"
 
 
+# The translation unit each kernel is compiled from (build.sh), by rocprof-name prefix.
+KERNEL_TU = (("dual_fill_ck_kernel", "ta_dual.hip"), ("dual_fill_kernel", "ta_dual.hip"),
+             ("flex_fill_kernel", "ta_flex.hip"), ("affine_", "ta_affine.hip"),
+             ("traceback_ck_kernel", "ta_walk_ck.hip"), ("fill_kernel", "ta_kernels.hip"),
+             ("traceback", "ta_kernels.hip"), ("format_runs_kernel", "ta_kernels.hip"))
+CSRC = os.path.join(ROOT, "bioinfo1_amd", "csrc")
+
+
+def kernel_src_hash(kernel, csrc=CSRC, build=os.path.join(ROOT, "build.sh")):
+    """sha256 (16 hex) over what a kernel's counters depend on: its translation
+    unit and every csrc header it includes (transitively), the planner and the
+    launch code (chunking, grids), and build.sh (flags, -D variants).  A counter
+    entry (profiles/{traffic,valu}_by_kernel.json) carries the hash of the source
+    it was measured on; bench.py quotes it only while the hash still matches."""
+    import re
+
+    tu = next((f for pre, f in KERNEL_TU if kernel.startswith(pre)), None)
+    if tu is None:
+        return None
+    seen, todo = [], [tu, "ta_planner.cpp", "ta_api.hip"]
+    while todo:
+        f = todo.pop(0)
+        path = os.path.join(csrc, f)
+        if f in seen or not os.path.exists(path):
+            continue
+        seen.append(f)
+        todo += re.findall(r'^#include "([^"/]+)"', open(path).read(), re.M)
+    h = hashlib.sha256()
+    for f in sorted(seen) + [None]:
+        h.update(open(os.path.join(csrc, f) if f else build, "rb").read())
+    return h.hexdigest()[:16]
+
+
 def profile_entry(name, kernel, tag):
-    """profiles/<name>: {"<kernel>|<workload tag>": {"value", "profile", ...}} --
-    counters of THIS kernel (rocprof name, dominant_kernel) on THIS workload,
-    written by scripts/prof_summary.py; None when not profiled."""
+    """profiles/<name>: {"<kernel>|<workload tag>": {"value", "profile", "src_hash", ...}}
+    -- counters of THIS kernel (rocprof name, dominant_kernel) on THIS workload,
+    written by scripts/prof_summary.py.  Returns (entry, None), or (None, why)
+    when there is no entry or it was measured on other source ("stale")."""
     e = load_profile(name, f"{kernel}|{tag}")
-    return e if isinstance(e, dict) else None
+    if not isinstance(e, dict):
+        return None, f"not profiled for {kernel} on this workload"
+    want = kernel_src_hash(kernel)
+    if e.get("src_hash") != want:
+        return None, (f"stale: profiles/{e.get('profile')}_pmc.json was measured on source {e.get('src_hash')}, "
+                      f"the loaded kernel is built from {want} (scripts/profile.sh + prof_summary.py to refresh)")
+    return e, None
 
 
 MODES_INV = {0: "kGlobal", 1: "kLocal", 2: "kSemi"}
@@ -817,13 +857,14 @@ def main_align(args, D):
         if affine:
             tag = "affine_" + tag
         kern = dominant_kernel(plan, mode, cigar, affine)
-        tr = profile_entry("traffic_by_kernel.json", kern, tag)
+        tr, tr_why = profile_entry("traffic_by_kernel.json", kern, tag)
         roof = {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": tr["value"] if tr else None,
                 "traffic_source": (f"rocprofv3 --pmc FETCH_SIZE x2 + WRITE_SIZE (separate passes) of {kern} on this "
                                    f"workload, bytes per step's fill: profiles/{tr['profile']}_pmc.json "
-                                   "(profiles/traffic_by_kernel.json; scripts/profile.sh)") if tr
-                else f"not profiled for {kern} on this workload",
+                                   f"(profiles/traffic_by_kernel.json, source {tr['src_hash']}; scripts/profile.sh)")
+                if tr else tr_why,
+                "src_hash": kernel_src_hash(kern),
                 "kernel": kern, "kernel_ms": round(fill_ms, 4),
                 "launches_per_step": plan.chunks,
                 "kernel_ms_per_dispatch": round(fill_ms / max(plan.chunks, 1), 4),
@@ -831,7 +872,7 @@ def main_align(args, D):
                 "per_launch_note": "one launch = the step's fill dispatches (one per chunk); traffic and "
                                    "ops/cell are rocprof per-dispatch averages x launches_per_step",
                 "note": "integer DP: VALU-bound, not HBM- or MFMA-bound (see valu)"}
-        ve = profile_entry("valu_by_kernel.json", kern, tag)
+        ve, ve_why = profile_entry("valu_by_kernel.json", kern, tag)
         ops = ve["value"] if ve else None
         kroof = (load_profile("valu_roof.json", "kernels") or {}).get(kern)
         peak = kroof["peak_lane_tops"] if kroof else VALU_PEAK_TOPS
@@ -842,7 +883,7 @@ def main_align(args, D):
                                "cycles per wave64 instruction") if kroof else "every instruction 4 cycles (fallback)",
                 "valu_ops_per_cell": ops,
                 "valu_ops_source": (f"rocprofv3 SQ_INSTS_VALU x 64 / cells of {kern} on this workload: "
-                                    f"profiles/{ve['profile']}_pmc.json") if ve else f"not profiled for {kern}",
+                                    f"profiles/{ve['profile']}_pmc.json, source {ve['src_hash']}") if ve else ve_why,
                 "achieved_lane_tops": round(batch.cells * ops / (fill_ms / 1e3) / 1e12, 2) if ops else None,
                 "frac": round(batch.cells * ops / (fill_ms / 1e3) / 1e12 / peak, 4) if ops else None}
         extra = {}

@@ -94,7 +94,12 @@ def main():
         if "FETCH_SIZE" in cs and "WRITE_SIZE" in cs:
             tr = int((2 * cs["FETCH_SIZE"] + cs["WRITE_SIZE"]) * 1024 * per_step)
         key = f"{short_name(k)}|{wtag}"
-        meta = {"profile": rtag, "kernel": k, "dispatches_per_step": per_step}
+        # the source the counters were measured on (bench.py quotes them only while it matches)
+        sys.path.insert(0, ROOT)
+        import bench
+
+        meta = {"profile": rtag, "kernel": k, "dispatches_per_step": per_step,
+                "src_hash": bench.kernel_src_hash(short_name(k))}
         if bl and (bl.get("roofline") or {}).get("kernel") not in (None, short_name(k)):
             print("WARNING: bench line names", bl["roofline"]["kernel"], "but the dominant PMC kernel is", k)
         merge(os.path.join(prof, "traffic_by_kernel.json"), key, dict(value=tr, **meta))
