@@ -621,7 +621,7 @@ def dominant_kernel(plan, mode, cigar, affine):
         return f"flex_fill_kernel<{mode}, {c}>"
     if plan.dual_pairs * 2 >= plan.P:
         if cigar and getattr(plan, "ck", False):
-            return "dual_fill_ck_kernel"  # (checkpoints instead of codes)
+            return f"dual_fill_ck_kernel<{mode}>"  # (checkpoints instead of codes)
         return f"dual_fill_kernel<{mode}, {c}, {'true' if (cigar and plan.blk) else 'false'}>"
     return f"fill_kernel<{mode}, {c}, false>"
 

@@ -57,6 +57,7 @@ constexpr bool kDualCk = true;
 #else
 constexpr bool kDualCk = false;
 #endif
+static_assert(!kDualCk || kDualStage != 0, "the checkpoint fill stages each step's bottom row in LDS");
 
 struct DualIo {
     const uint8_t* Q[2];
@@ -680,11 +681,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_
 }
 #if defined(TA_DUAL_BLK) && TA_DUAL_CK
 // the checkpoint fill under a name of its own (rocprof, profiles/*_by_kernel.json)
+template <int MODE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_DUAL_WAVES))) void dual_fill_ck_kernel(FillArgs a) {
-#ifdef TA_FILL_PRIO
-    __builtin_amdgcn_s_setprio(TA_FILL_PRIO);
-#endif
-    dual_fill_body<TA_DUAL_MODE, true, true>(a);
+    dual_fill_body<MODE, true, true>(a);
 }
 #endif
 
@@ -733,7 +732,8 @@ __global__ void dual_combine_kernel(FillArgs a) {
 
 #ifdef TA_DUAL_MODE
 #if defined(TA_DUAL_BLK) && TA_DUAL_CK
-hipError_t launch_dual_ck(const FillArgs& a, hipStream_t s) {
+template <>
+hipError_t launch_dual_ck<TA_DUAL_MODE>(const FillArgs& a, hipStream_t s) {
 #elif defined(TA_DUAL_BLK)
 hipError_t launch_dual_blk(const FillArgs& a, hipStream_t s) {
 #else
@@ -742,13 +742,17 @@ hipError_t launch_dual_mode<TA_DUAL_MODE, (TA_DUAL_CIGAR != 0)>(const FillArgs& 
 #endif
     if (!a.count) return hipSuccess;
 #if defined(TA_DUAL_BLK) && TA_DUAL_CK  // (the checkpoint layout)
-    hipLaunchKernelGGL(dual_fill_ck_kernel, dual_grid(a.ticket ? a.n_tasks : a.count), dim3(kBlock), 0, s, a);
+    hipLaunchKernelGGL(dual_fill_ck_kernel<TA_DUAL_MODE>, dual_grid(a.ticket ? a.n_tasks : a.count), dim3(kBlock), 0, s,
+                       a);
 #elif defined(TA_DUAL_BLK)  // (its own translation unit: the blocked-layout local fill)
     hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, true, true>), dual_grid(a.ticket ? a.n_tasks : a.count),
                        dim3(kBlock), 0, s, a);
 #else
+#if TA_DUAL_CIGAR
+    if (a.blk == 2) return launch_dual_ck<TA_DUAL_MODE>(a, s);  // (checkpoint plans: any mode)
+#endif
 #if TA_DUAL_MODE == 1 && TA_DUAL_CIGAR
-    if (a.blk) return a.blk == 2 ? launch_dual_ck(a, s) : launch_dual_blk(a, s);
+    if (a.blk) return launch_dual_blk(a, s);
 #endif
     hipLaunchKernelGGL((dual_fill_kernel<TA_DUAL_MODE, TA_DUAL_CIGAR != 0>), dual_grid(a.ticket ? a.n_tasks : a.count),
                        dim3(kBlock), 0, s, a);

@@ -175,11 +175,13 @@ template <int MODE, bool CIGAR>
 hipError_t launch_dual_mode(const FillArgs& a, hipStream_t s);
 // the local CIGAR dual fill in the blocked code layout (ta_dual.hip, TA_DUAL_BLK)
 hipError_t launch_dual_blk(const FillArgs& a, hipStream_t s);
-// ... and in the checkpoint layout (TA_DUAL_BLK + TA_DUAL_CK; FillArgs.blk == 2)
+// ... and in the checkpoint layout of any mode (TA_DUAL_BLK + TA_DUAL_CK, a translation
+// unit per mode; FillArgs.blk == 2)
+template <int MODE>
 hipError_t launch_dual_ck(const FillArgs& a, hipStream_t s);
-// The recomputing local walks of checkpoint plans (ta_walk_ck.hip; TraceArgs.blk == 2),
-// then the fallback walk of the handed-back pairs; format_runs_kernel follows.
-hipError_t launch_walk_ck(const TraceArgs& a, hipStream_t s);
+// The recomputing walks of checkpoint plans (ta_walk_ck.hip; TraceArgs.blk == 2), then
+// the fallback walk of the handed-back pairs; format_runs_kernel follows.
+hipError_t launch_walk_ck(int mode, const TraceArgs& a, hipStream_t s);
 // Flexible two-pair fill (ta_flex.hip, global / semi-global): a.order holds 2
 // pair ids per wave, the larger n first; both with the same pass count and
 // n mod 16; rebased int16 values, so any length fits.

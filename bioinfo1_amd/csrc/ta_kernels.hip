@@ -1055,13 +1055,14 @@ hipError_t launch_traceback(int mode, const TraceArgs& a, hipStream_t s, int gro
         hipLaunchKernelGGL(traceback_group_kernel<32>, grid_for((a.count + 1) / 2), b, 0, s, a);
         return hipGetLastError();
     }
+    if (group == 64 && a.blk == 2) {  // recomputing walks over checkpoints (ta_walk_ck.hip), any mode
+        const hipError_t e = launch_walk_ck(mode, a, s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(format_runs_kernel, g, b, 0, s, a);
+        return hipGetLastError();
+    }
     if (mode == kLocal && group == 64) {  // band walks (blocked layout), one lane per pair
-        if (a.blk == 2) {  // ... or recomputing walks over checkpoints (ta_walk_ck.hip)
-            const hipError_t e = launch_walk_ck(a, s);
-            if (e != hipSuccess) return e;
-        } else {
-            hipLaunchKernelGGL(traceback_band_kernel, dim3((a.count + kWave - 1) / kWave), dim3(kWave), 0, s, a);
-        }
+        hipLaunchKernelGGL(traceback_band_kernel, dim3((a.count + kWave - 1) / kWave), dim3(kWave), 0, s, a);
         hipLaunchKernelGGL(format_runs_kernel, g, b, 0, s, a);
         return hipGetLastError();
     }

@@ -240,9 +240,10 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     // lone pair, rather than in the int32 fill: a drop-in batch of 3 x 1 kb went
     // 1.12 -> 0.78 ms with the packed fill and walk for all of its pairs
     // (profiles/bench/r05_batch_latency.txt).
-    // (tiny pairs keep the int32 fill: alone, its one fused launch is the shortest)
+    // (tiny pairs keep the int32 fill: alone, its one fused launch is the shortest --
+    // unless checkpoints are forced, kPlanCk: the tests' way into the checkpoint walks)
     auto lone_dual = [&](uint32_t p) {
-        return dual && (uint64_t)qlen[p] * tlen[p] >= 4096 && n_passes(qlen[p]) < 64 &&
+        return dual && ((uint64_t)qlen[p] * tlen[p] >= 4096 || (flags & kPlanCk)) && n_passes(qlen[p]) < 64 &&
                fits_int16(type, qlen[p], tlen[p], match, mismatch, gap);
     };
     for (uint32_t k = 0; k < n_pairs;) {
@@ -325,8 +326,23 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     // 1 kb, scripts/exp/batch_latency.py, profiles/bench/r05_batch_latency.txt)
     bool all_dual = !units.empty();
     for (const Unit& u : units) all_dual = all_dual && u.kind == 1;
-    pl.blk = want_cigar && type == kLocal && all_dual && short_pairs && n_pairs >= 8 && mag < (1ull << 22) &&
-             !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2));
+    // Checkpoints save the fill ~0.3 of its time but the recomputing walk is a
+    // longer chain per pair than the band walk (one window per 16 rows): they pay
+    // once the cells per unit of the longest path pass ~2.5e6 (1 kb pairs: from
+    // ~5,000 pairs on; 8 to 4,096 measured slower, profiles/bench/r05_ck_batches.txt).
+    uint64_t cells = 0, longest = 1;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        cells += (uint64_t)qlen[p] * tlen[p];
+        longest = std::max<uint64_t>(longest, (uint64_t)qlen[p] + tlen[p]);
+    }
+    const bool ck_size = (flags & kPlanCk) || cells >= 2500000ull * longest;
+    // Global / semi-global plans of equal-shape couples (config 5) take checkpoints
+    // and recomputing walks by the same rule, whatever their lengths: their walks end
+    // on row 0 / column 0 (ta_walk_ck.hip) and need no cost, so no gap-sign condition.
+    const bool edge_ck = want_cigar && type != kLocal && all_dual && mag < (1ull << 22) && ck_size &&
+                         !(flags & (kPlanNoCk | kPlanNoBlk | kPlanWalk1 | kPlanWalk2));
+    pl.blk = (want_cigar && type == kLocal && all_dual && short_pairs && n_pairs >= 8 && mag < (1ull << 22) &&
+              !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2))) || edge_ck;
     // Multi-pass int32 pairs run one wave per (pair, pass) like the packed
     // fills (their passes overlap instead of following each other on one
     // wave); the walk then runs in the traceback kernel.
@@ -414,21 +430,12 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     // config 2; their runs are clipped to 32 cells, so batches of long pairs (long
     // M runs) keep the one-pair walk (config 3 local: 4.1 vs 6.3 ms).  24-bit
     // multiplies of the scores in the run walks.
-    if (pl.blk) pl.walk_group = gap <= 0 ? 64 : 0;  // (a positive gap lowers the cost in gap runs: one-pair walk)
+    // (local: a positive gap lowers the cost in gap runs -- the one-pair walk)
+    if (pl.blk) pl.walk_group = (gap <= 0 || type != kLocal) ? 64 : 0;
     else if ((flags & kPlanWalk1) || mag >= (1ull << 22) || !short_pairs) pl.walk_group = 0;
     else if ((flags & kPlanWalk2) || gap < -128 || gap > 127) pl.walk_group = 32;
     else pl.walk_group = 16;
-    // Checkpoints save the fill ~0.3 of its time but the recomputing walk is a
-    // longer chain per pair than the band walk (one window per 16 rows): they pay
-    // once the cells per unit of the longest path pass ~2.5e6 (1 kb pairs: from
-    // ~5,000 pairs on; 8 to 4,096 measured slower, profiles/bench/r05_ck_batches.txt).
-    uint64_t cells = 0, longest = 1;
-    for (uint32_t p = 0; p < n_pairs; ++p) {
-        cells += (uint64_t)qlen[p] * tlen[p];
-        longest = std::max<uint64_t>(longest, (uint64_t)qlen[p] + tlen[p]);
-    }
-    pl.ck = pl.blk && pl.walk_group == 64 && !(flags & kPlanNoCk) &&
-            ((flags & kPlanCk) || cells >= 2500000ull * longest);
+    pl.ck = pl.blk && pl.walk_group == 64 && !(flags & kPlanNoCk) && ck_size;
     // (Each dual wave walking its own two pairs right after its fill measured
     // slower: config 2 3.10 ms vs 2.19 + 0.65; the walk inherits the fill's
     // register allocation and all waves finish their fills together anyway.)

@@ -92,6 +92,7 @@ __device__ __forceinline__ void ck_wave_sync() { __builtin_amdgcn_fence(__ATOMIC
 // The pairs the dual fill handed back ('-' bytes; usually none), one wave per
 // pair in the one-pair walk over their blocked codes -- here rather than in a
 // launch of its own, whose count only the device knows.
+template <int MODE>
 __device__ __forceinline__ void ck_fallback_walks(const TraceArgs& a, int lane) {
     if (!a.fb_count) return;
     const uint32_t nfb = *a.fb_count;
@@ -101,7 +102,7 @@ __device__ __forceinline__ void ck_fallback_walks(const TraceArgs& a, int lane) 
         uint64_t st;
         uint32_t len;
         const WalkSeq seq{a.qbytes + a.qoff[q], a.tbytes + a.toff[q], a.score[q], a.match, a.mismatch, a.gap};
-        traceback_pair<kLocal>(a.ptrs + a.ptr_off[q], qn, qm, a.goal_i[q], a.goal_j[q], a.slots + a.slot_off[q],
+        traceback_pair<MODE>(a.ptrs + a.ptr_off[q], qn, qm, a.goal_i[q], a.goal_j[q], a.slots + a.slot_off[q],
                                cigar_slot_bytes(qn, qm), lane, &st, &len, seq, true);
         if (lane == 0) {
             a.cigar_start[q] = a.slot_off[q] + st;
@@ -128,9 +129,11 @@ struct CkPair {
 
 // (<= 128 VGPRs: beside the next batch's fill -- 96 VGPRs a wave -- a walk wave then displaces
 // one fill wave of its SIMD, not two)
+template <int MODE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void traceback_ck_kernel(TraceArgs a) {
+    constexpr bool LOCAL = MODE == kLocal;
     __shared__ CkGroup groups[kWavesPerBlock * kCkGroups];
-    __shared__ uint32_t gtab[256];  // ck_gain_table of every byte value
+    __shared__ uint32_t gtab[256];  // per byte value: local: ck_gain_table; global / semi: mismatch_table
     // a latency-bound chain: beside the next batch's fill (align.DevicePipeline)
     // its instructions go first at the SIMD's issue arbiter (measured neutral)
     __builtin_amdgcn_s_setprio(3);
@@ -141,6 +144,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int mag = max(max(max(ma, -ma), max(mi, -mi)), max(max(gap, -gap), 1));
     const int B = mag + 1;   // bias: values H + gap + B >= 1
     const int GB = gap + B;  // the value of a cell with H = 0
+    // global / semi: the values are the fill's own S = H - ma j + gap (j - i) (ta_dual.hip,
+    // int16 by fits_int16): the diagonal gain is (s - ma), the up one 0, the left one 2 gap - ma;
+    // row 0 holds S(0, j) = R0 j, column 0 S(i, 0) = C0 i (:81-92)
+    const int R0 = (MODE == kGlobal ? gap : 0) - ma + gap, C0 = MODE == kGlobal ? 0 : -gap;
     CkPair S[2];
     int ci[2], cj[2];        // the walk's current cell of each pair
     bool live[2];
@@ -162,12 +169,12 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             c.m = a.tlen[c.p];
             ci[h] = (int)a.goal_i[c.p];
             cj[h] = (int)a.goal_j[c.p];
-            H = a.score[c.p];
+            H = LOCAL ? a.score[c.p] : min(ci[h], cj[h]);  // (global / semi: a walk to row 0 or column 0)
             c.P = reinterpret_cast<const uint16_t*>(a.ptrs + a.ptr_off[c.p]);
             c.Q += a.qoff[c.p];
             c.T += a.toff[c.p];
         }
-        const int off3 = c.has ? local_max3_offset(c.n, c.m, ma, mi, gap) : -1;  // the fill's frame (ck_decode)
+        const int off3 = (LOCAL && c.has) ? local_max3_offset(c.n, c.m, ma, mi, gap) : -1;  // the fill's frame (ck_decode)
         c.off = off3 >= 0 ? off3 : 0;
         c.dl = off3 >= 0 ? zstep + 16 : 0;
         c.nb = blk_count(c.m);
@@ -180,6 +187,25 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint32_t cap = 2 * mnm - 1;  // the walk's room (ta_internal.h band_runs_off)
     uint32_t nev = 0, kI = 0, windows = 0;       // events listed; the pending I run (across windows)
     bool mdone = !(hh ? live[1] : live[0]);      // (a pair with score 0 has nothing to walk)
+    // runs of one op in events of at most 8192 (the count fields: 14 bits for I, 16 for D)
+    auto emit = [&](bool ins, uint32_t c) {
+        while (c) {
+            const uint32_t k = min(c, 8192u);
+            if (lw == 0) rout[nev] = ins ? (k << 2) | 1u : (k << 16) | 3u;
+            ++nev;
+            c -= k;
+        }
+    };
+    if (!LOCAL && mhas) {
+        // semi-global: the goal's trailing run to column m / row n comes last in the CIGAR,
+        // first in the walk (:306-315); a goal on row 0 / column 0 is only the boundary run
+        const int gi = hh ? ci[1] : ci[0], gj = hh ? cj[1] : cj[0];
+        const uint32_t n = hh ? S[1].n : S[0].n, m = hh ? S[1].m : S[0].m;
+        if (MODE == kSemi && (uint32_t)gi == n && (uint32_t)gj < m) emit(true, m - (uint32_t)gj);
+        else if (MODE == kSemi && (uint32_t)gj == m && (uint32_t)gi < n) emit(false, n - (uint32_t)gi);
+        if (gi < 1) emit(true, (uint32_t)gj);
+        else if (gj < 1) emit(false, (uint32_t)gi);
+    }
     const uint32_t SA2 = rep16(ma - gap), GAP2 = rep16(gap), KD2 = rep16(mi - ma), B2 = rep16(B), Z2 = rep16(B + 1);
     const uint32_t GB2 = rep16(GB);
     uint32_t ONE = 0x00010001u;
@@ -187,8 +213,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const bool first = lg == 0;
     // TAB windows need both gains (s - gap) in [-128, 127]
     const int ua = ma - gap + 128, ub = mi - gap + 128;
-    const bool tab_ok = (uint32_t)ua < 256u && (uint32_t)ub < 256u;
-    gtab[threadIdx.x] = ck_gain_table(threadIdx.x, ua, ub);  // (kBlock == 256: one byte value per thread)
+    const bool tab_ok = !LOCAL || ((uint32_t)ua < 256u && (uint32_t)ub < 256u);
+    const uint32_t GL2 = rep16(2 * gap - ma), KE2 = rep16(mi - ma);  // (global / semi gains)
+    gtab[threadIdx.x] = LOCAL ? ck_gain_table(threadIdx.x, ua, ub) : mismatch_table(threadIdx.x);  // (kBlock == 256)
     static_assert(kBlock == 256, "one gain table entry per thread");
     __syncthreads();
     uint32_t KN = swar_k(-128);
@@ -269,20 +296,40 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             const uint32_t ct = ((uint32_t)CT[0] & 0xFFFFu) | ((uint32_t)CT[1] << 16);
             const uint32_t l0 = __builtin_amdgcn_perm(vl[1], vl[0], 0x05040100u);  // row 2 lg of A, B
             const uint32_t l1 = __builtin_amdgcn_perm(vl[1], vl[0], 0x07060302u);  // row 2 lg + 1
-            gl0 = vsel(mL0, pk_lshr4(pk_add(l0, cl)), GB2);
-            gl1 = vsel(mL1, pk_lshr4(pk_add(l1, pk_add(cl, ONE))), GB2);
-            // column 0 (c0 = 0, x = 0): H = 0
+            // column 0 (c0 = 0, x = 0): the boundary
             const uint32_t m0 = mT & (lg == 0 ? ((c0[0] > 0 ? 0xFFFFu : 0u) | (c0[1] > 0 ? 0xFFFF0000u : 0u)) : ~0u);
-            const uint32_t dx = rep16(-8 * zstep);  // the decode constant moves by -zstep per column
-            uint32_t ctq = ct;
+            if constexpr (LOCAL) {
+                gl0 = vsel(mL0, pk_lshr4(pk_add(l0, cl)), GB2);
+                gl1 = vsel(mL1, pk_lshr4(pk_add(l1, pk_add(cl, ONE))), GB2);
+                const uint32_t dx = rep16(-8 * zstep);  // the decode constant moves by -zstep per column
+                uint32_t ctq = ct;
 #pragma unroll
-            for (int q = 0; q < 5; ++q) {
-                // (columns past W: H = 0, see ck_gain_table)
-                const int x = lg + 8 * q;
-                const uint32_t mw = (x <= W[0] ? 0xFFFFu : 0u) | (x <= W[1] ? 0xFFFF0000u : 0u);
-                const uint32_t s = vt[0][q] | (vt[1][q] << 16);
-                G.top[x] = vsel((q == 0 ? m0 : mT) & mw, pk_lshr4(pk_add(s, ctq)), GB2);
-                ctq = pk_add(ctq, dx);
+                for (int q = 0; q < 5; ++q) {
+                    // (columns past W: H = 0, see ck_gain_table)
+                    const int x = lg + 8 * q;
+                    const uint32_t mw = (x <= W[0] ? 0xFFFFu : 0u) | (x <= W[1] ? 0xFFFF0000u : 0u);
+                    const uint32_t s = vt[0][q] | (vt[1][q] << 16);
+                    G.top[x] = vsel((q == 0 ? m0 : mT) & mw, pk_lshr4(pk_add(s, ctq)), GB2);
+                    ctq = pk_add(ctq, dx);
+                }
+            } else {
+                // the stored S values as they are; the boundaries computed: column 0 S(i, 0) =
+                // C0 i, row 0 S(0, j) = R0 j (stripe 0's top row)
+                const int ir0 = 16 * g[0] + 2 * lg + 1, ir1 = 16 * g[1] + 2 * lg + 1;
+                const uint32_t cb = ((uint32_t)(C0 * ir0) & 0xFFFFu) | ((uint32_t)(C0 * ir1) << 16);
+                const uint32_t mE = (live[0] && c0[0] > 0 ? 0xFFFFu : 0u) | (live[1] && c0[1] > 0 ? 0xFFFF0000u : 0u);
+                gl0 = vsel(mE, l0, cb);
+                gl1 = vsel(mE, l1, pk_add(cb, rep16(C0)));
+                const uint32_t rowb = ((uint32_t)(R0 * (c0[0] + lg)) & 0xFFFFu) | ((uint32_t)(R0 * (c0[1] + lg)) << 16);
+                const uint32_t colb = ((uint32_t)(C0 * 16 * g[0]) & 0xFFFFu) | ((uint32_t)(C0 * 16 * g[1]) << 16);
+                uint32_t rq = rowb;
+#pragma unroll
+                for (int q = 0; q < 5; ++q) {
+                    const uint32_t s = vt[0][q] | (vt[1][q] << 16);
+                    const uint32_t alt = q == 0 ? vsel(mT, colb, rq) : rq;  // (q > 0: column > 0)
+                    G.top[lg + 8 * q] = vsel(q == 0 ? m0 : mT, s, alt);
+                    rq = pk_add(rq, rep16(8 * R0));
+                }
             }
         }
         // the window's sweep kind (wave-uniform): TAB when every query row is A, C, G, T
@@ -316,6 +363,32 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 else bv[s].x = tbl[kb + s].x;
             }
             uint32_t a0 = acc[0][kb / 8], a1 = acc[1][kb / 8], a2 = acc[2][kb / 8];
+            if constexpr (!LOCAL) {
+                // global / semi: S values, no clamp; D and I signs of saturating differences
+                // (S and its candidates are int16 -- fits_int16 -- their differences need not be)
+#pragma unroll
+                for (int s = 0; s < 8; ++s) {
+                    const uint32_t dpp = (uint32_t)__builtin_amdgcn_mov_dpp((int)gl1, 0x111, 0xF, 0xF, true);
+                    const uint32_t up0 = first ? tv[s] : dpp;
+                    const uint32_t e0 = TAB ? mismatch_flags(bv[s].x, bv[s].y, q0) : pk_min_u16(q0 ^ bv[s].x, ONE);
+                    const uint32_t e1 = TAB ? mismatch_flags(bv[s].x, bv[s].y, q1) : pk_min_u16(q1 ^ bv[s].x, ONE);
+                    const uint32_t dg0 = pk_mad_i16(e0, KE2, upp), lf0 = pk_add(gl0, GL2);
+                    const uint32_t m10 = pk_max(dg0, lf0), hn0 = pk_max(m10, up0);
+                    const uint32_t dg1 = pk_mad_i16(e1, KE2, gl0), lf1 = pk_add(gl1, GL2);
+                    const uint32_t m11 = pk_max(dg1, lf1), hn1 = pk_max(m11, hn0);
+                    const uint32_t mk = 0x01010101u << (7 - s);
+                    a0 = bfi(mk, sign_bytes(pk_sub_sat(m10, up0), pk_sub_sat(dg0, lf0)), a0);  // [I0A, I0B, D0A, D0B]
+                    a1 = bfi(mk, sign_bytes(pk_sub_sat(m11, hn0), pk_sub_sat(dg1, lf1)), a1);  // [I1A, I1B, D1A, D1B]
+                    if (kb >= 8 || kb + s >= lg) {
+                        gl0 = hn0;
+                        gl1 = hn1;
+                    }
+                    upp = up0;
+                }
+                acc[0][kb / 8] = a0;
+                acc[1][kb / 8] = a1;
+                return;
+            }
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
                 // the first row: up from the lane above's second row (row_shr:1; a
@@ -376,7 +449,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         for (int h = 0; h < 2; ++h) {
             const uint32_t i0 = word(acc[0], (uint32_t)h, W[h]), d0 = word(acc[0], 2u + h, W[h]);
             const uint32_t i1 = word(acc[1], (uint32_t)h, W[h]), d1 = word(acc[1], 2u + h, W[h]);
-            const uint32_t z0 = word(acc[2], (uint32_t)h, W[h]), z1 = word(acc[2], 2u + h, W[h]);
+            const uint32_t z0 = LOCAL ? word(acc[2], (uint32_t)h, W[h]) : 0u, z1 = LOCAL ? word(acc[2], 2u + h, W[h]) : 0u;
             G.row[h][2 * lg] = make_uint4(~i0 | d0, d0, z0, 0u);
             G.row[h][2 * lg + 1] = make_uint4(~i1 | d1, d1, z1, 0u);
         }
@@ -390,14 +463,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // depends on and lists each step's record; the events come from the records.
         const int mr = hh ? r[1] : r[0], mW = hh ? W[1] : W[0], mg = hh ? g[1] : g[0], mc0 = hh ? c0[1] : c0[0];
         const bool mlive = hh ? live[1] : live[0];
-        const bool room = nev + 2u * (uint32_t)(mr + 1) + 1u <= cap;  // (<= 2 events per row step, + an I-run split)
+        // (<= 2 events per row step, + an I-run split; global / semi: + the boundary run's)
+        const bool room = nev + 2u * (uint32_t)(mr + 1) + (LOCAL ? 1u : 8u) <= cap;
         uint32_t wl = (mlive && room) ? 1u : 0u, zdone = 0, nrec = 0, pos = 0;
         int rr = mr;
         const uint4* rp = &G.row[hh][rr - 1];  // the row a move up reaches (a walk only moves up)
         uint32_t* recs = G.rec[hh];
         uint32_t* recp = recs;                  // step k's record at recs[k] (the steps of a live walk are its records)
         auto row_step = [&](const uint4& w4, uint32_t* rec) {
-            const uint32_t zero = (w4.z >> pos) & 1u;
+            const uint32_t zero = LOCAL ? (w4.z >> pos) & 1u : 0u;
             // (NI's bit W is set when W < 32; a run to the edge of a 32-column window finds no
             // NI bit, hence the 33rd bit and the bound)
             const uint32_t run = min((uint32_t)__builtin_ctzll((uint64_t)(w4.x >> pos) | (1ull << 32)), (uint32_t)mW - pos);
@@ -481,6 +555,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             }
             ++windows;
             const bool done = zdone || mi_ < 1 || mj < 1;  // row 0 / column 0: H = 0
+            if (!LOCAL && done) {
+                // the boundary: INSERTs along row 0, DELETEs down column 0 (:81-92) -- after an
+                // I run that reached column 0 in this window
+                emit(true, kI);
+                kI = 0;
+                if (mi_ < 1) emit(true, (uint32_t)mj);
+                else emit(false, (uint32_t)mi_);
+            }
             mdone = done;
             ml = !done && room && windows <= mnm + 16u;
         }
@@ -503,14 +585,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (!mdone) atomicOr(a.err, kErrWalkCap);
         a.cigar_len[mp] = nev;  // the event count, for format_runs_kernel
     }
-    ck_fallback_walks(a, lane);
+    ck_fallback_walks<MODE>(a, lane);
 }
 
 }  // namespace
 
-hipError_t launch_walk_ck(const TraceArgs& a, hipStream_t s) {
-    const uint32_t per_block = kWavesPerBlock * kCkGroups * 2;
-    hipLaunchKernelGGL(traceback_ck_kernel, dim3((a.count + per_block - 1) / per_block), dim3(kBlock), 0, s, a);
+hipError_t launch_walk_ck(int mode, const TraceArgs& a, hipStream_t s) {
+    const dim3 g((a.count + kWavesPerBlock * kCkGroups * 2 - 1) / (kWavesPerBlock * kCkGroups * 2)), b(kBlock);
+    switch (mode) {
+        case kLocal: hipLaunchKernelGGL(traceback_ck_kernel<kLocal>, g, b, 0, s, a); break;
+        case kGlobal: hipLaunchKernelGGL(traceback_ck_kernel<kGlobal>, g, b, 0, s, a); break;
+        case kSemi: hipLaunchKernelGGL(traceback_ck_kernel<kSemi>, g, b, 0, s, a); break;
+        default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

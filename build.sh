@@ -37,8 +37,10 @@ for m in 0 1 2; do
 done
 # the blocked-layout local fill (band walks) in a translation unit of its own
 cc "$B/ta_dual_blk.o" "$CS/ta_dual.hip" "$HIPCC" "${FLAGS[@]}" -DTA_DUAL_MODE=1 -DTA_DUAL_CIGAR=1 -DTA_DUAL_BLK -c "$CS/ta_dual.hip"
-# ... in the checkpoint layout, and the recomputing walks over it
-cc "$B/ta_dual_ck.o" "$CS/ta_dual.hip" "$HIPCC" "${FLAGS[@]}" -DTA_DUAL_MODE=1 -DTA_DUAL_CIGAR=1 -DTA_DUAL_BLK -DTA_DUAL_CK=1 -c "$CS/ta_dual.hip"
+# ... in the checkpoint layout (every mode), and the recomputing walks over it
+for m in 0 1 2; do
+  cc "$B/ta_dual_ck_$m.o" "$CS/ta_dual.hip" "$HIPCC" "${FLAGS[@]}" -DTA_DUAL_MODE=$m -DTA_DUAL_CIGAR=1 -DTA_DUAL_BLK -DTA_DUAL_CK=1 -c "$CS/ta_dual.hip"
+done
 cc "$B/ta_walk_ck.o" "$CS/ta_walk_ck.hip" "$HIPCC" "${FLAGS[@]}" -c "$CS/ta_walk_ck.hip"
 for m in 0 1 2; do
   for c in 0 1; do
@@ -64,7 +66,7 @@ done
 cc "$B/tm_main.o" "$CS/tm_main.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp"
 fi
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_dual_blk.o" "$B/ta_dual_ck.o" "$B/ta_walk_ck.o" "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_server.o" "$B/ta_planner.o" "$B/shim.o" \
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_dual_blk.o" "$B"/ta_dual_ck_{0,1,2}.o "$B/ta_walk_ck.o" "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_server.o" "$B/ta_planner.o" "$B/shim.o" \
   -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$OUT"
 if [ "${TA_LIB_ONLY:-0}" = 1 ]; then echo "built $OUT"; exit 0; fi
 PKG="$ROOT/bioinfo1_amd"

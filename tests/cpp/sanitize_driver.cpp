@@ -296,15 +296,20 @@ void check_small_batches() {
                         std::printf("small batch %u x %ux%u type %d flags %u: %zu chunks\n", P, sh[0], sh[1], type, flags,
                                     pl.chunks.size());
                     // every pair in the packed kernels (an odd one coupled with itself) when it fits
-                    // int16 and is not tiny; band walks (blocked layout) from 8 local pairs up
-                    const bool packed = (uint64_t)sh[0] * sh[1] >= 4096 && ta::fits_int16(type, sh[0], sh[1], 1, -1, -1);
+                    // int16 and is not tiny (or TA_PLAN_CK); band walks (blocked layout) from 8 local pairs up
+                    const bool packed = ((uint64_t)sh[0] * sh[1] >= 4096 || flags == 512u) &&
+                                        ta::fits_int16(type, sh[0], sh[1], 1, -1, -1);
                     // (n_dual_pairs counts two per couple, a self-coupled pair included)
                     if (packed) CHECK(pl.singles.empty() && pl.n_dual_pairs == 2 * ((P + 1) / 2));
                     // (tiny pairs of an even batch still couple with each other; only a lone one stays int32)
                     const bool all_packed = ta::fits_int16(type, sh[0], sh[1], 1, -1, -1) && (packed || P % 2 == 0);
-                    CHECK(pl.blk == (all_packed && type == ta::kLocal && P >= 8 && flags != 128u && sh[0] + sh[1] <= 6000));
+                    // global / semi: checkpoints (blocked region sizes) whenever they are taken
+                    const bool edge_ck = all_packed && type != ta::kLocal && flags == 512u;
+                    CHECK(pl.blk == ((all_packed && type == ta::kLocal && P >= 8 && flags != 128u && sh[0] + sh[1] <= 6000) ||
+                                     edge_ck));
                     // checkpoints and recomputing walks: small batches only with TA_PLAN_CK (gap -1 <= 0)
                     CHECK(pl.ck == (pl.blk && flags == 512u));
+                    if (pl.ck) CHECK(pl.walk_group == 64);
                 }
 }
 

@@ -14,20 +14,20 @@ import bench  # noqa: E402
 
 
 def test_matching_hash_is_quoted_and_mismatch_is_stale(monkeypatch):
-    h = bench.kernel_src_hash("dual_fill_ck_kernel")
+    h = bench.kernel_src_hash("dual_fill_ck_kernel<1>")
     assert h and len(h) == 16
     entry = {"value": 123, "profile": "rX_cfg2", "src_hash": h}
     monkeypatch.setattr(bench, "load_profile", lambda name, tag: dict(entry))
-    e, why = bench.profile_entry("traffic_by_kernel.json", "dual_fill_ck_kernel", "t")
+    e, why = bench.profile_entry("traffic_by_kernel.json", "dual_fill_ck_kernel<1>", "t")
     assert e["value"] == 123 and why is None
     entry["src_hash"] = "0" * 16
-    e, why = bench.profile_entry("traffic_by_kernel.json", "dual_fill_ck_kernel", "t")
+    e, why = bench.profile_entry("traffic_by_kernel.json", "dual_fill_ck_kernel<1>", "t")
     assert e is None and why.startswith("stale")
     del entry["src_hash"]  # entries from before the hashes: stale too
-    e, why = bench.profile_entry("valu_by_kernel.json", "dual_fill_ck_kernel", "t")
+    e, why = bench.profile_entry("valu_by_kernel.json", "dual_fill_ck_kernel<1>", "t")
     assert e is None and why.startswith("stale")
     monkeypatch.setattr(bench, "load_profile", lambda name, tag: None)
-    e, why = bench.profile_entry("valu_by_kernel.json", "dual_fill_ck_kernel", "t")
+    e, why = bench.profile_entry("valu_by_kernel.json", "dual_fill_ck_kernel<1>", "t")
     assert e is None and why.startswith("not profiled")
 
 

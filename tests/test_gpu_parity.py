@@ -564,6 +564,89 @@ def test_ck_walk(aligner, oracle, sc):
         assert got.cigar(p) == want.cigar(p), (sc, p, b.qlen[p], b.tlen[p])
 
 
+@pytest.mark.parametrize("name", ["g1k_global", "s1k_semi", "cfg5_semi_sample"])
+def test_digest_ck_edge(aligner, name):
+    """Global and semi-global digests of the reference through checkpoint plans
+    (TA_PLAN_CK: the dual fill stores checkpoints, the global / semi-global
+    recomputing walk of ta_walk_ck.hip walks to row 0 / column 0): bit-exact."""
+    meta, d = load_digest(name)
+    batch = digest_batch(name)
+    sc = (meta["match"], meta["mismatch"], meta["gap"])
+    plan = DevicePlan(aligner, batch, meta["type"], *sc, True, flags=TA_PLAN_CK)
+    assert plan.ck and plan.blk and plan.walk == 64, (plan.ck, plan.blk, plan.walk)
+    plan.close()
+    r = run_plan(aligner, batch, meta["type"], sc, True, TA_PLAN_CK)
+    np.testing.assert_array_equal(r.scores, d["scores"])
+    np.testing.assert_array_equal(r.target_begins, d["target_begins"])
+    np.testing.assert_array_equal(r.cigar_lens, d["cigar_lens"])
+    sha, crc = cigar_digest(r, batch.n_pairs)
+    np.testing.assert_array_equal(crc, d["cigar_crc32"])
+    assert sha == meta["cigar_sha256"]
+
+
+@pytest.mark.parametrize("mode", [0, 2])
+def test_ck_walk_edge_kats(aligner, kat_cases, random_cases, mode):
+    """Every known-answer case and random pair of the reference in global /
+    semi-global mode through checkpoint plans (TA_PLAN_CK; lone pairs run
+    coupled with themselves): the worked examples, the semi trailing runs
+    (5I1M1I2M2D, 7I1M8D), goals on row 0 / column 0, '-' bytes (handed back to
+    the one-pair walk), lowercase and N."""
+    groups = {}
+    for c in kat_cases + random_cases:
+        if c["type"] == mode and not c["error"] and c["query"] and c["target"]:
+            groups.setdefault((c["match"], c["mismatch"], c["gap"]), []).append(c)
+    ck = n = 0
+    for sc, cs in groups.items():
+        b = synth.from_pairs([(bytes.fromhex(c["query"]), bytes.fromhex(c["target"])) for c in cs])
+        flags = TA_PLAN_CK | TA_PLAN_NO_FLEX  # (every pair a dual couple, coupled with itself)
+        plan = DevicePlan(aligner, b, mode, *sc, True, flags=flags)
+        ck += plan.ck
+        plan.close()
+        r = run_plan(aligner, b, mode, sc, True, flags)
+        for k, c in enumerate(cs):
+            got = (int(r.scores[k]), r.cigar(k), int(r.target_begins[k]))
+            assert got == (c["score"], bytes.fromhex(c["cigar"]), c["target_begin"]), (c["source"], c, got)
+            n += 1
+    assert ck >= 3 and n > 50, (ck, n)
+
+
+@pytest.mark.parametrize("mode,sc", [(m, s) for m in (0, 2) for s in ((1, -1, -1), (2, -3, -1), (3, 4, 0), (2, -1, 2))])
+def test_ck_walk_edge(aligner, oracle, mode, sc):
+    """Global / semi-global recomputing walks over checkpoints against the
+    oracle: odd numbers of couples per shape (self-coupled pairs), one to three
+    query passes, long I runs and D runs (inserted blocks that match nothing)
+    that cross windows, stripes and a pass edge, semi goals in the last row and
+    the last column, and related pairs."""
+    rng = np.random.default_rng(0xED6E + 11 * mode + 7 * sc[0] - sc[1])
+    al = np.frombuffer(b"ACGT", np.uint8)
+    rnd = lambda k: al[rng.integers(4, size=k)].tobytes()  # noqa: E731
+    pairs = []
+    for n, m, cnt in ((300, 280, 9), (1030, 990, 5), (2100, 700, 3), (40, 600, 3), (700, 64, 3)):
+        for k in range(cnt):
+            core = rnd(min(n, m) - 100 if min(n, m) > 200 else min(n, m) // 2)
+            gapb = b"N" * (40 + 23 * k)
+            if k % 3 == 0:  # an insertion in the target: an I run
+                q, t = core, core[: len(core) // 2] + gapb + core[len(core) // 2:]
+            elif k % 3 == 1:  # a deletion: a D run
+                q, t = core[: len(core) // 3] + gapb + core[len(core) // 3:], core
+            else:
+                q, t = rnd(n), rnd(m)
+            q, t = (q + rnd(max(0, n - len(q))))[:n], (t + rnd(max(0, m - len(t))))[:m]
+            pairs.append((q, t))
+    rb = synth.related_batch(9, 900, 900, seed=0xED6F)
+    pairs += [(rb.query(p), rb.target(p)) for p in range(rb.n_pairs)]
+    b = synth.from_pairs(pairs)
+    plan = DevicePlan(aligner, b, mode, *sc, True, flags=TA_PLAN_CK)
+    assert plan.ck and plan.walk == 64, (plan.blk, plan.ck, plan.walk)
+    plan.close()
+    want = oracle.align_batch(b, mode, *sc, True)
+    got = run_plan(aligner, b, mode, sc, True, TA_PLAN_CK)
+    np.testing.assert_array_equal(got.scores, want.scores)
+    np.testing.assert_array_equal(got.target_begins, want.target_begins)
+    for p in range(b.n_pairs):
+        assert got.cigar(p) == want.cigar(p), (mode, sc, p, b.qlen[p], b.tlen[p])
+
+
 def test_local_walk_long_runs(aligner, oracle):
     """Local paths with long gap and match runs (past the group walk's 32-cell
     clip and the one-pair walk's 64-cell windows) across pass and tile edges
