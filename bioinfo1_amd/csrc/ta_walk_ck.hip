@@ -187,12 +187,17 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint32_t cap = 2 * mnm - 1;  // the walk's room (ta_internal.h band_runs_off)
     uint32_t nev = 0, kI = 0, windows = 0;       // events listed; the pending I run (across windows)
     bool mdone = !(hh ? live[1] : live[0]);      // (a pair with score 0 has nothing to walk)
-    // runs of one op in events of at most 8192 (the count fields: 14 bits for I, 16 for D)
+    // runs of one op in events of at most 8192 (the count fields: 14 bits for I, 16 for D);
+    // never past the pair's room (a walk moves >= 1 cell per event of its records, so with the
+    // trailing and boundary runs its events stay <= n + m + 4 <= cap for n + m >= 3; a full
+    // room marks the walk unfinished, the plan's error word)
+    bool capped = false;
     auto emit = [&](bool ins, uint32_t c) {
         while (c) {
             const uint32_t k = min(c, 8192u);
-            if (lw == 0) rout[nev] = ins ? (k << 2) | 1u : (k << 16) | 3u;
-            ++nev;
+            capped |= nev >= cap;
+            if (lw == 0 && nev < cap) rout[nev] = ins ? (k << 2) | 1u : (k << 16) | 3u;
+            nev += nev < cap ? 1u : 0u;
             c -= k;
         }
     };
@@ -463,8 +468,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // depends on and lists each step's record; the events come from the records.
         const int mr = hh ? r[1] : r[0], mW = hh ? W[1] : W[0], mg = hh ? g[1] : g[0], mc0 = hh ? c0[1] : c0[0];
         const bool mlive = hh ? live[1] : live[0];
-        // (<= 2 events per row step, + an I-run split; global / semi: + the boundary run's)
-        const bool room = nev + 2u * (uint32_t)(mr + 1) + (LOCAL ? 1u : 8u) <= cap;
+        // (<= 2 events per row step, + an I-run split; the boundary runs check their own room)
+        const bool room = nev + 2u * (uint32_t)(mr + 1) + 1u <= cap;
         uint32_t wl = (mlive && room) ? 1u : 0u, zdone = 0, nrec = 0, pos = 0;
         int rr = mr;
         const uint4* rp = &G.row[hh][rr - 1];  // the row a move up reaches (a walk only moves up)
@@ -582,7 +587,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // (a walk stopped by the event cap or the window bound before a cell with
         // H = 0 -- never a correct one, its events <= n + m -- would hand over a
         // truncated CIGAR: the plan's error word says so)
-        if (!mdone) atomicOr(a.err, kErrWalkCap);
+        if (!mdone || capped) atomicOr(a.err, kErrWalkCap);
         a.cigar_len[mp] = nev;  // the event count, for format_runs_kernel
     }
     ck_fallback_walks<MODE>(a, lane);
