@@ -1086,24 +1086,32 @@ def main_dropin(args):
     """Single-call team::Align (the reference mapper's calling pattern) through
     our drop-in library vs the reference's own Align, same harness, same pairs."""
     res = {}
-    # amd: the drop-in as shipped (pairs up to 4096 x 16384 on the resident single-pair server);
-    # amd_batch_path: the same library with TEAM_ALIGN_SERVER=0 (concurrent calls combined into batches)
-    for name, exe, env in (("amd", os.path.join(ROOT, "build", "dropin_amd"), {}),
-                           ("amd_batch_path", os.path.join(ROOT, "build", "dropin_amd"), {"TEAM_ALIGN_SERVER": "0"}),
-                           ("reference", os.path.join(ROOT, "oracle", "_ref", "dropin_ref"), {})):
+    # amd: the drop-in as shipped (pairs up to 4096 x 16384 on the resident single-pair server), run as
+    # a plain library user runs it -- the process default of hardware queues, 4 on the box;
+    # amd_batch_path: the same library with TEAM_ALIGN_SERVER=0 (concurrent calls combined into batches);
+    # amd_queues16: one thread under GPU_MAX_HW_QUEUES=16 (what bench.py sets for its pipelines),
+    # the r05 cause of the slower 5x9 round trip
+    amd = os.path.join(ROOT, "build", "dropin_amd")
+    for name, exe, env, threads in (("amd", amd, {}, (1, 8, 16)),
+                                    ("amd_batch_path", amd, {"TEAM_ALIGN_SERVER": "0"}, (1, 8, 16)),
+                                    ("amd_queues16", amd, {"GPU_MAX_HW_QUEUES": "16"}, (1,)),
+                                    ("reference", os.path.join(ROOT, "oracle", "_ref", "dropin_ref"), {}, (1, 8, 16))):
         if not os.path.exists(exe):
             continue
         rows = []
-        for thr in (1, 8, 16):  # 16: the host cores a GPU box grants this job
+        for thr in threads:  # 16: the host cores a GPU box grants this job
+            e = _dropin_env({k: v for k, v in env.items() if k != "GPU_MAX_HW_QUEUES"})
+            e.update({k: v for k, v in env.items() if k == "GPU_MAX_HW_QUEUES"})
             p = subprocess.run([exe, str(thr), "1.0", "5x9,200x200,1000x1000", str(MODES[args.mode or "local"])],
-                               capture_output=True, text=True, timeout=300, check=True, env=_dropin_env(env))
+                               capture_output=True, text=True, timeout=300, check=True, env=e)
             rows += [json.loads(x) for x in p.stdout.splitlines() if x.startswith("{")]
         res[name] = rows
     same = None
     if "amd" in res and "reference" in res:
         key = lambda r: (r["shape"], r["threads"])  # noqa: E731
         ref = {key(r): r["score_checksum"] for r in res["reference"]}
-        same = all(ref.get(key(r)) == r["score_checksum"] for v in ("amd", "amd_batch_path") for r in res.get(v, []))
+        same = all(ref.get(key(r)) == r["score_checksum"] for v in ("amd", "amd_batch_path", "amd_queues16")
+                   for r in res.get(v, []))
     print(json.dumps({"metric": "team::Align single-call throughput (drop-in, one pair per call)", "unit": "calls/s",
                       "mode": args.mode or "local", "score_checksums_equal": same, "results": res}), flush=True)
 
