@@ -507,22 +507,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             recp += 2;
         }
         ck_wave_sync();
-        // events of the records, two per record: an I run (with the run carried from
-        // the previous window on the first record) and the D or M move; a record that
-        // ran to the window's edge carries its run to the next window.  Records
-        // 4 lw .. 4 lw + 3 per lane.
+        // events of the records: an I run (with the run carried from the previous window
+        // on the first record) and the D or M move; a record that ran to the window's edge
+        // carries its run to the next window.  Consecutive M moves with no I run between
+        // them are one event, written at the run's last record (the formatter's work
+        // goes with the events: ~1,000 a config-2 pair, about half of them M moves that
+        // continue an M run).  Records 4 lw .. 4 lw + 3 per lane; the pair's M-move and
+        // no-I-run masks over its 16 records are OR-ed over the pair's 4 lanes.
         {
-            uint32_t ev[8], ne = 0;
+            uint32_t rcs[4], mm = 0, zm = 0;
 #pragma unroll
             for (int h = 0; h < 4; ++h) {
                 const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h;
-                const uint32_t rc = k < nrec ? recs[k] : 0x200u;  // (past the list: no event)
+                rcs[h] = k < nrec ? recs[k] : 0x200u;  // (past the list: no event)
+                const uint32_t runI = (rcs[h] & 63u) + (k == 0 ? kI : 0u);
+                mm |= ((rcs[h] & 0x300u) == 0 ? 1u : 0u) << k;  // an M move
+                zm |= (runI == 0 ? 1u : 0u) << k;
+            }
+            const uint32_t o1 = quad<0xB1>(mm), z1 = quad<0xB1>(zm);  // quad_perm [1, 0, 3, 2]
+            mm |= o1;
+            zm |= z1;
+            const uint32_t o2 = quad<0x4E>(mm), z2 = quad<0x4E>(zm);  // quad_perm [2, 3, 0, 1]
+            mm |= o2;
+            zm |= z2;
+            const uint32_t cont = mm & zm & (mm << 1);  // record k continues record k - 1's M run
+            uint32_t ev[8], ne = 0;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h, rc = rcs[h];
                 const uint32_t runI = (rc & 63u) + (k == 0 ? kI : 0u);
                 const bool ed = rc & 0x200u, iev = !ed && runI > 0;
+                // an M run ending here: its first record is the last one at or below k that
+                // does not continue a run (bit 0 never does)
+                const uint32_t below = ~cont & ((2u << k) - 1u);
+                const uint32_t mcount = k + 1u - (31u - (uint32_t)__builtin_clz(below));
+                const bool mend = ((mm >> k) & 1u) && !((cont >> (k + 1u)) & 1u);
                 ev[2 * h] = (runI << 2) | 1u;
-                ev[2 * h + 1] = (rc & 0x100u) ? ((1u << 16) | 3u) : 4u;  // D: a D run of 1, no move; M
+                ev[2 * h + 1] = (rc & 0x100u) ? ((1u << 16) | 3u) : (mcount << 2);  // D: a D run of 1, no move; M run
                 ne |= (iev ? 1u : 0u) << (2 * h);
-                ne |= (ed ? 0u : 1u) << (2 * h + 1);
+                ne |= (!ed && ((rc & 0x100u) || mend) ? 1u : 0u) << (2 * h + 1);
             }
             // exclusive prefix of the lane's event counts over the pair's 4 lanes
             const uint32_t cnt = (uint32_t)__builtin_popcount(ne);

@@ -213,13 +213,24 @@ def kernel_events_walk(H, D, I, i, j):
             rr -= mv
             zdone |= wl & zero
             wl = mv & (1 if rr >= 0 else 0) & (1 if pos < W else 0)
+        # M moves with no I run between them: one event at the run's last record
+        mm = zm = 0
+        for k, rc in enumerate(recs):
+            runI = (rc & 63) + (kI if k == 0 else 0)
+            mm |= (1 if (rc & 0x300) == 0 else 0) << k
+            zm |= (1 if runI == 0 else 0) << k
+        cont = mm & zm & (mm << 1)
         for k, rc in enumerate(recs):
             runI = (rc & 63) + (kI if k == 0 else 0)
             if rc & 0x200:
                 continue
             if runI:
                 ev.append((runI << 2) | 1)
-            ev.append(((1 << 16) | 3) if rc & 0x100 else 4)
+            if rc & 0x100:
+                ev.append((1 << 16) | 3)
+            elif not (cont >> (k + 1)) & 1:
+                below = ~cont & ((2 << k) - 1)
+                ev.append((k + 1 - (below.bit_length() - 1)) << 2)
         if recs:
             last = recs[-1]
             kI = ((last & 63) + (kI if len(recs) == 1 else 0)) if last & 0x200 else 0
