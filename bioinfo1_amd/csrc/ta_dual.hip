@@ -121,7 +121,13 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     if constexpr (!M3) off = 0;
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const int init = (MODE == kGlobal) ? gap : 0;
-    const int zstep = 1 - 16 * ma;  // local: S(0, j) = zstep * j
+    constexpr bool CK = BLK && kDualCk;
+    constexpr bool CODES = CIGAR && !CK;
+    // EQ (M3 without codes): the equal-gain frame z = -1 (ta_layout.h local_max3_z):
+    // H = max(diag + 16s - 2, max(left, up) + 16gap - 1, clamp), the diagonal gain
+    // from a byte table (CLS) -- five instructions a row instead of six
+    constexpr bool EQ = M3 && !CODES;
+    const int zstep = local_max3_z(ma, EQ);  // local: S(0, j) = zstep * j
     const uint32_t KD = rep16(LOCAL ? 16 * (mi - ma) : (mi - ma));
     // left gain (no '-' in these targets); global / semi: the up gain is 0 (the
     // -gap*i term of S), so the left one carries gap twice
@@ -131,12 +137,18 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // every value and candidate of the M3 frame lies in [0, 0x7BFF]
     // (local_max3_offset), so the low half never borrows from the high one
     constexpr bool SW = M3 && TA_SWAR;
-    constexpr bool CK = BLK && kDualCk;
-    constexpr bool CODES = CIGAR && !CK;
     uint32_t GLk = swar_k(LOCAL ? 16 * gap + zstep : 2 * gap - ma), GUGk = swar_k(16 * gap - 1);
     asm volatile("" : "+s"(GLk), "+s"(GUGk));  // SGPR operands (a literal would double the encoding)
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // opaque: keeps v_pk_min_u16 (see pk_min_u16)
+    // EQ: the diagonal gain 16s - 2 as table bytes + 128 (class_table: byte k = ub, or
+    // ua for the class-k letter), added with the bias as ONE v_add3_u32 (the walk's TAB
+    // sweep, ta_walk_ck.hip); without the tables (not CLS) the mismatch delta then + GM
+    const uint32_t ua = (uint32_t)(16 * ma - 2 + 128), ub = (uint32_t)(16 * mi - 2 + 128);
+    const uint32_t T0 = ub * 0x01010101u, TX = ua ^ ub;
+    const uint32_t GM = rep16(16 * ma - 2);
+    uint32_t KN = swar_k(-128);
+    asm volatile("" : "+s"(KN));
     const uint32_t Tmax = pass_steps(m);
     const uint32_t row_base = pass * kPassRows;
     const uint32_t nrows = min((uint32_t)kPassRows, n - row_base);
@@ -269,7 +281,10 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         const uint32_t prev = recv;
         recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
         if constexpr (UZ) recv = pk_add(recv, D2);
-        if constexpr (CLS) {
+        if constexpr (CLS && EQ) {
+            tA = (uint32_t)wave_shr1((int)class_table((wa >> sh) & 0xFFu, T0, TX), (int)tA);
+            tB = (uint32_t)wave_shr1((int)class_table((wb >> sh) & 0xFFu, T0, TX), (int)tB);
+        } else if constexpr (CLS) {
             tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
             tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
         } else {
@@ -291,7 +306,13 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 if constexpr (CLS) return mismatch_flags(tA, tB, q2[r]);
                 else return pk_min_u16(q2[r] ^ tc2, ONE);
             };
-            uint32_t dnext = pk_mad_i16(e_of(0), KD, prev);
+            // the diagonal candidate of row r from the value diagonally above it
+            auto diag_of = [&](int r, uint32_t dv) -> uint32_t {
+                if constexpr (EQ && CLS) return dv + mismatch_flags(tA, tB, q2[r]) + KN;  // (v_add3_u32)
+                else if constexpr (EQ) return pk_add(pk_mad_i16(e_of(r), KD, dv), GM);
+                else return pk_mad_i16(e_of(r), KD, dv);
+            };
+            uint32_t dnext = diag_of(0, prev);
             uint32_t upv = recv;
             uint32_t Z = Zp;
             // M3: the clamp bases of rows 2k, 2k+1 in the halves of W[k] (op_sel picks one)
@@ -306,8 +327,17 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
                 constexpr int r = decltype(rc)::value;
                 const uint32_t old = H2[r];
                 const uint32_t diag = dnext;
+                if constexpr (r + 1 < R) dnext = diag_of(r + 1, old);
+                if constexpr (EQ) {
+                    // left and up share the gain: max first, one add (M3 values are in
+                    // [0, 0x7BFF], so the max is the integers')
+                    const uint32_t lu = pk_max(old, upv);
+                    const uint32_t hv = pk_max3_pos_bc<r & 1>(diag, SW ? swar_add(lu, GLk) : pk_add(lu, GL), W[r / 2]);
+                    H2[r] = hv;
+                    upv = hv;
+                    return;
+                }
                 const uint32_t left = SW ? swar_add(old, GLk) : pk_add(old, GL);
-                if constexpr (r + 1 < R) dnext = pk_mad_i16(e_of(r + 1), KD, old);
                 const uint32_t up = LOCAL ? (SW ? swar_add(upv, GUGk) : pk_add(upv, GUG)) : upv;
                 const uint32_t m1 = pk_max(diag, left);
                 uint32_t hv;
@@ -479,7 +509,9 @@ __device__ __forceinline__ DualOut dual_pass_nv(const FillArgs& a, const DualIo&
     const uint32_t nrows = min((uint32_t)kPassRows, n - pass * kPassRows);
     const uint32_t nv = nrows - ((nrows + kRows - 1) / kRows - 1) * kRows;
     if constexpr (MODE == kLocal) {
-        const int off = local_max3_offset(n, m, a.match, a.mismatch, a.gap);  // wave-uniform
+        // (the fills without codes use the equal-gain frame, dual_pass EQ)
+        constexpr bool eq = !CIGAR || (BLK && kDualCk);
+        const int off = local_max3_offset(n, m, a.match, a.mismatch, a.gap, eq);  // wave-uniform
         if (off >= 0) {
             if (nv == kRows)
                 return dual_pass<MODE, CIGAR, kRows, true, CLS, BLK>(a, io, n, m, pass, last_pass, lane, off);

@@ -25,24 +25,34 @@ constexpr int kBlock = kWave * kWavesPerBlock;
 enum Mode : int { kGlobal = 0, kLocal = 1, kSemi = 2 };
 
 // Local dual fill (ta_dual.hip) with three-input maxima: its biased values
-// S = 16H + z*j - i (z = 1 - 16*ma) and every candidate, shifted by the
-// returned offset, lie in [0, 0x7BFF] -- non-negative int16 whose bit
-// patterns, read as f16, are finite and ordered like the integers, so
-// v_pk_maximum3_f16 takes their max.  Bounds: a local path into (i, j) has at
-// most min(i, j) diagonal steps and i + j gap steps, so
+// S = 16H + z*j - i and every candidate, shifted by the returned offset, lie in
+// [0, 0x7BFF] -- non-negative int16 whose bit patterns, read as f16, are
+// finite and ordered like the integers, so v_pk_maximum3_f16 takes their max.
+// Two frames (local_max3_z): z = 1 - 16*ma, where a match's diagonal gain is 0
+// (the fills that store codes), and the equal-gain frame z = -1 (eq: the
+// checkpoint and score-only fills), where the up and left gains are both
+// 16*gap - 1 -- one gain add on the larger of the two -- and the diagonal gain
+// 16*s - 2 comes from a byte table (local_eq_gains: s in [-7, 8]).
+// Bounds: a local path into (i, j) has at most min(i, j) diagonal steps and
+// i + j gap steps, so
 //   H <= hs*j + gp*(i + j)   (hs = max(0, ma, mi), gp = max(0, gap))
 //   S <= (16hs + 16gp + z)*j + (16gp - 1)*i,   S >= z*j - i (the clamp),
 // rows up to n + 15 (the last lane's padding rows), candidates one step
 // (<= 16*mag) below the clamp; lane l holds S + (z + 16)*l (its frame, so
 // that the clamp bases of a step are the same in every lane), l < 64.
 // -1: does not fit (the max/max kernel runs).
-TA_HD inline int local_max3_offset(uint32_t n, uint32_t m, int ma, int mi, int gap) {
+TA_HD inline bool local_eq_gains(int ma, int mi) {
+    return ma >= -7 && ma <= 8 && mi >= -7 && mi <= 8;  // 16 s - 2 + 128 in [0, 255]
+}
+TA_HD inline int local_max3_z(int ma, bool eq) { return eq ? -1 : 1 - 16 * ma; }
+TA_HD inline int local_max3_offset(uint32_t n, uint32_t m, int ma, int mi, int gap, bool eq = false) {
+    if (eq && !local_eq_gains(ma, mi)) return -1;
     const long long N = (long long)n + 16, M = m;
     const long long ama = ma < 0 ? -ma : ma, ami = mi < 0 ? -mi : mi, ag = gap < 0 ? -gap : gap;
     const long long mag = ama > ami ? (ama > ag ? ama : ag) : (ami > ag ? ami : ag);
     const long long hs = ma > mi ? (ma > 0 ? ma : 0) : (mi > 0 ? mi : 0);
     const long long gp = gap > 0 ? gap : 0;
-    const long long z = 1 - 16LL * ma;
+    const long long z = local_max3_z(ma, eq);
     const long long cj = 16 * hs + 16 * gp + z, ci = 16 * gp - 1;
     const long long fl = 63 * (z + 16);  // lane frame
     const long long hi = (cj > 0 ? cj * M : 0) + (ci > 0 ? ci * N : 0) + 32 * (mag + 1) + (fl > 0 ? fl : 0);
@@ -103,9 +113,10 @@ TA_HD inline uint64_t ck_col_index(uint32_t pass, uint32_t b, uint32_t lane, uin
     return (((uint64_t)pass * 2 + 1) * nb * kWave + (uint64_t)b * kWave + lane) * kBlkSteps + r;
 }
 // H of the cell (i, j) (1-based) from the packed value s the local dual fill
-// held for it in lane l of its pass: s = off + 16 H + (1 - 16 ma) j - i + dl l,
-// with off = local_max3_offset and dl = 17 - 16 ma in the three-input-max frame
-// (off >= 0; ta_dual.hip M3 / UZ), off = dl = 0 otherwise.
+// held for it in lane l of its pass: s = off + 16 H + z j - i + dl l, with
+// off = local_max3_offset(.., eq = true), z = -1 and dl = z + 16 = 15 in the
+// checkpoint fill's three-input-max frame (off >= 0; ta_dual.hip M3 / UZ / EQ),
+// off = dl = 0 and z = 1 - 16 ma otherwise.
 TA_HD inline int ck_decode(int s, int off, int zstep, int dl, int i, int j, int l) {
     return (s - off - zstep * j + i - dl * l) >> 4;
 }

@@ -73,12 +73,15 @@ __device__ __forceinline__ uint32_t max3_reduce(const uint32_t* v) {
 __device__ __forceinline__ bool is_acgt(uint32_t c) {
     return c == ((0x47544341u >> (8u * ((c >> 1) & 3u))) & 0xFFu);
 }
-__device__ __forceinline__ uint32_t mismatch_table(uint32_t c) {
-    // (a select of the bit, not a bool shifted: keeps the whole table on the SALU)
+// The general table: byte k = mis, or hit when c is the class-k letter, as
+// t0 = mis * 0x01010101 and x = hit ^ mis (the local equal-gain frame's gain
+// bytes 16 s - 2 + 128, ta_layout.h local_eq_gains).
+__device__ __forceinline__ uint32_t class_table(uint32_t c, uint32_t t0, uint32_t x) {
+    // (a select of the bits, not a bool shifted: keeps the whole table on the SALU)
     const uint32_t sh = 8u * ((c >> 1) & 3u);
-    const uint32_t bit = 1u << sh;
-    return 0x01010101u ^ ((c == ((0x47544341u >> sh) & 0xFFu)) ? bit : 0u);
+    return t0 ^ ((c == ((0x47544341u >> sh) & 0xFFu)) ? x << sh : 0u);
 }
+__device__ __forceinline__ uint32_t mismatch_table(uint32_t c) { return class_table(c, 0x01010101u, 1u); }
 __device__ __forceinline__ uint32_t row_selector(uint32_t qa, uint32_t qb) {
     return ((qa >> 1) & 3u) | 0x0C00u | ((4u + ((qb >> 1) & 3u)) << 16) | 0x0C000000u;
 }

@@ -66,10 +66,11 @@ struct CkGroup {
     uint2 tb[8 + 8 * kCkBlocks + 1];
     // (after top / tb: the walk reads the row above row 0 -- up to 18 rows -- of
     // walkers that already left, from inside the group)
-    uint4 row[2][16];                    // per pair and row: NI, D, H = 0 window words
+    uint2 row[2][16];                    // per pair and row: NI, D window words
     uint32_t rec[2][16];                 // per pair: the window's row steps
+    uint8_t qb[2][16];                   // local: per pair, the query bytes of the stripe's rows
 };
-static_assert(offsetof(CkGroup, row) >= 18 * sizeof(uint4), "room above a walker's row 0");
+static_assert(offsetof(CkGroup, row) >= 18 * sizeof(uint2), "room above a walker's row 0");
 
 // TAB windows (every query row of both pairs is A, C, G or T; ta_packed.h
 // mismatch_table): the diagonal gain of a cell is a byte of its column's gain
@@ -120,7 +121,7 @@ __device__ __forceinline__ uint32_t quad(uint32_t v) {
 // Per-pair constants, held by every lane of the pair's group.
 struct CkPair {
     uint32_t p, n, m, nb;
-    int off, dl;
+    int off, z, dl;  // the fill's frame (ta_layout.h ck_decode)
     const uint16_t* P;
     const uint8_t* Q;
     const uint8_t* T;
@@ -140,7 +141,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int lane = (int)threadIdx.x & 63, lg = lane & 7, hh = lg >> 2, lw = lg & 3;
     CkGroup& G = groups[threadIdx.x >> 3];
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
-    const int zstep = 1 - 16 * ma;
     const int mag = max(max(max(ma, -ma), max(mi, -mi)), max(max(gap, -gap), 1));
     const int B = mag + 1;   // bias: values H + gap + B >= 1
     const int GB = gap + B;  // the value of a cell with H = 0
@@ -150,6 +150,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const int R0 = (MODE == kGlobal ? gap : 0) - ma + gap, C0 = MODE == kGlobal ? 0 : -gap;
     CkPair S[2];
     int ci[2], cj[2];        // the walk's current cell of each pair
+    int hc[2];               // local: its H (the cost the walk carries)
     bool live[2];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -174,11 +175,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             c.Q += a.qoff[c.p];
             c.T += a.toff[c.p];
         }
-        const int off3 = (LOCAL && c.has) ? local_max3_offset(c.n, c.m, ma, mi, gap) : -1;  // the fill's frame (ck_decode)
+        // the checkpoint fill's frame (ck_decode): the equal-gain one with three-input maxima
+        const int off3 = (LOCAL && c.has) ? local_max3_offset(c.n, c.m, ma, mi, gap, true) : -1;
         c.off = off3 >= 0 ? off3 : 0;
-        c.dl = off3 >= 0 ? zstep + 16 : 0;
+        c.z = local_max3_z(ma, off3 >= 0);
+        c.dl = off3 >= 0 ? c.z + 16 : 0;
         c.nb = blk_count(c.m);
         live[h] = c.has && H > 0;  // a positive score has its goal at i, j >= 1
+        hc[h] = H;
     }
     // the walker's own pair (lanes 0-3: pair A, 4-7: pair B)
     const bool mhas = hh ? S[1].has : S[0].has;
@@ -187,6 +191,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     const uint32_t cap = 2 * mnm - 1;  // the walk's room (ta_internal.h band_runs_off)
     uint32_t nev = 0, kI = 0, windows = 0;       // events listed; the pending I run (across windows)
     bool mdone = !(hh ? live[1] : live[0]);      // (a pair with score 0 has nothing to walk)
+    int mcost = hh ? hc[1] : hc[0];              // local: H of the walker's cell
     // runs of one op in events of at most 8192 (the count fields: 14 bits for I, 16 for D);
     // never past the pair's room (a walk moves >= 1 cell per event of its records, so with the
     // trailing and boundary runs its events stay <= n + m + 4 <= cap for n + m >= 3; a full
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         if (gi < 1) emit(true, (uint32_t)gj);
         else if (gj < 1) emit(false, (uint32_t)gi);
     }
-    const uint32_t SA2 = rep16(ma - gap), GAP2 = rep16(gap), KD2 = rep16(mi - ma), B2 = rep16(B), Z2 = rep16(B + 1);
+    const uint32_t SA2 = rep16(ma - gap), GAP2 = rep16(gap), KD2 = rep16(mi - ma), B2 = rep16(B);
     const uint32_t GB2 = rep16(GB);
     uint32_t ONE = 0x00010001u;
     asm volatile("" : "+s"(ONE));  // (see ta_packed.h pk_min_u16)
@@ -225,9 +230,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     uint32_t KN = swar_k(-128);
     asm volatile("" : "+s"(KN));
-    uint32_t acc[3][kCkBlocks];
+    uint32_t acc[2][kCkBlocks];
 #pragma unroll
-    for (int b = 0; b < kCkBlocks; ++b) acc[0][b] = acc[1][b] = acc[2][b] = 0u;
+    for (int b = 0; b < kCkBlocks; ++b) acc[0][b] = acc[1][b] = 0u;
 
     while (ballot(live[0] || live[1])) {
         // ---- both pairs' windows: loads first (one wait for all), then the decodes
@@ -276,7 +281,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             vq[h][0] = live[h] ? c.Q[min(ir, qn)] : 0x41u;
             vq[h][1] = live[h] ? c.Q[min(ir + 1u, qn)] : 0x41u;
         }
-        // decodes (ta_layout.h ck_decode, plus gap + B): v = (s - off - zstep j + i - dl l) / 16 + gap + B
+        // decodes (ta_layout.h ck_decode, plus gap + B): v = (s - off - z j + i - dl l) / 16 + gap + B
         // is exact in 16-bit wrap-around arithmetic ((s + C) mod 2^16 = 16 (H + gap + B) < 2^16),
         // so both pairs decode together: one packed add of C and one packed shift
         uint32_t gl0, gl1, q0, q1, mT = 0, mL0 = 0, mL1 = 0;
@@ -288,8 +293,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 const CkPair& c = S[h];
                 const int l = g[h] & 63, lu = (g[h] - 1) & 63;
                 const int ir = 16 * g[h] + 2 * lg + 1;  // the lane's first row
-                CL[h] = 16 * GB - c.off - zstep * c0[h] + ir - c.dl * l;
-                CT[h] = 16 * GB - c.off - zstep * (c0[h] + lg) + 16 * g[h] - c.dl * lu;
+                CL[h] = 16 * GB - c.off - c.z * c0[h] + ir - c.dl * l;
+                CT[h] = 16 * GB - c.off - c.z * (c0[h] + lg) + 16 * g[h] - c.dl * lu;
                 // (rows past n: H = 0 too, see ck_gain_table)
                 const bool hl = live[h] && c0[h] > 0;
                 mL0 |= (hl && ir <= (int)c.n) ? 0xFFFFu << (16 * h) : 0u;
@@ -306,7 +311,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             if constexpr (LOCAL) {
                 gl0 = vsel(mL0, pk_lshr4(pk_add(l0, cl)), GB2);
                 gl1 = vsel(mL1, pk_lshr4(pk_add(l1, pk_add(cl, ONE))), GB2);
-                const uint32_t dx = rep16(-8 * zstep);  // the decode constant moves by -zstep per column
+                // the decode constant moves by -z per column
+                const uint32_t dx = ((uint32_t)(-8 * S[0].z) & 0xFFFFu) | ((uint32_t)(-8 * S[1].z) << 16);
                 uint32_t ctq = ct;
 #pragma unroll
                 for (int q = 0; q < 5; ++q) {
@@ -336,6 +342,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                     rq = pk_add(rq, rep16(8 * R0));
                 }
             }
+        }
+        if constexpr (LOCAL) {
+#pragma unroll
+            for (int h = 0; h < 2; ++h) *reinterpret_cast<uint16_t*>(&G.qb[h][2 * lg]) = (uint16_t)(vq[h][0] | (vq[h][1] << 8));
         }
         // the window's sweep kind (wave-uniform): TAB when every query row is A, C, G, T
         const bool tab = tab_ok && !ballot(!acgt);
@@ -367,7 +377,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 if constexpr (TAB) bv[s] = tbl[kb + s];
                 else bv[s].x = tbl[kb + s].x;
             }
-            uint32_t a0 = acc[0][kb / 8], a1 = acc[1][kb / 8], a2 = acc[2][kb / 8];
+            uint32_t a0 = acc[0][kb / 8], a1 = acc[1][kb / 8];
             if constexpr (!LOCAL) {
                 // global / semi: S values, no clamp; D and I signs of saturating differences
                 // (S and its candidates are int16 -- fits_int16 -- their differences need not be)
@@ -412,11 +422,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 const uint32_t m11 = pk_max(dg1, gl1);
                 const uint32_t hn1 = pk_max3_pos(m11, gn0, B2);
                 const uint32_t gn1 = pk_add(hn1, GAP2);
-                // signs: D (up beats both), I (left beats the diagonal), H = 0
+                // signs: D (up beats both), I (left beats the diagonal)
                 const uint32_t mk = 0x01010101u << (7 - s);
                 a0 = bfi(mk, sign_bytes(pk_sub(m10, up0), pk_sub(dg0, gl0)), a0);   // [I0A, I0B, D0A, D0B]
                 a1 = bfi(mk, sign_bytes(pk_sub(m11, gn0), pk_sub(dg1, gl1)), a1);   // [I1A, I1B, D1A, D1B]
-                a2 = bfi(mk, sign_bytes(pk_sub(hn1, Z2), pk_sub(hn0, Z2)), a2);     // [Z0A, Z0B, Z1A, Z1B]
                 if (kb >= 8 || kb + s >= lg) {  // (ramp: columns <= 0 keep the checkpoint)
                     gl0 = gn0;
                     gl1 = gn1;
@@ -425,7 +434,6 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             }
             acc[0][kb / 8] = a0;
             acc[1][kb / 8] = a1;
-            acc[2][kb / 8] = a2;
         };
         auto sweep = [&](auto tab_tag) {
             block(std::integral_constant<int, 0>{}, tab_tag);
@@ -454,47 +462,45 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         for (int h = 0; h < 2; ++h) {
             const uint32_t i0 = word(acc[0], (uint32_t)h, W[h]), d0 = word(acc[0], 2u + h, W[h]);
             const uint32_t i1 = word(acc[1], (uint32_t)h, W[h]), d1 = word(acc[1], 2u + h, W[h]);
-            const uint32_t z0 = LOCAL ? word(acc[2], (uint32_t)h, W[h]) : 0u, z1 = LOCAL ? word(acc[2], 2u + h, W[h]) : 0u;
-            G.row[h][2 * lg] = make_uint4(~i0 | d0, d0, z0, 0u);
-            G.row[h][2 * lg + 1] = make_uint4(~i1 | d1, d1, z1, 0u);
+            G.row[h][2 * lg] = make_uint2(~i0 | d0, d0);
+            G.row[h][2 * lg + 1] = make_uint2(~i1 | d1, d1);
         }
         ck_wave_sync();
 
         // ---- the walk across the window, one row per step (lanes 0-3: pair A, 4-7: pair B):
-        // stop on a cell with H = 0 (its cost, :20-28); else the I run from the current
-        // column (up to the first NI bit, at most to column 0), then
-        // the D or M move out of the row -- or, when the run reaches column c0, on in the
-        // next window.  Flags as 0 / 1 integers; the loop keeps only what the next step
-        // depends on and lists each step's record; the events come from the records.
+        // the I run from the current column (up to the first NI bit, at most to column 0),
+        // then the D or M move out of the row -- or, when the run reaches column c0, on in
+        // the next window.  Flags as 0 / 1 integers; the loop keeps only what the next step
+        // depends on and lists each step's record; the events come from the records.  A local
+        // walk also stops on the first cell with H = 0 (its cost, :20-28): found after the
+        // loop from the records, whose moves fix the cost of every cell on the path.
         const int mr = hh ? r[1] : r[0], mW = hh ? W[1] : W[0], mg = hh ? g[1] : g[0], mc0 = hh ? c0[1] : c0[0];
         const bool mlive = hh ? live[1] : live[0];
         // (<= 2 events per row step, + an I-run split; the boundary runs check their own room)
         const bool room = nev + 2u * (uint32_t)(mr + 1) + 1u <= cap;
-        uint32_t wl = (mlive && room) ? 1u : 0u, zdone = 0, nrec = 0, pos = 0;
+        uint32_t wl = (mlive && room) ? 1u : 0u, nrec = 0, pos = 0;
         int rr = mr;
-        const uint4* rp = &G.row[hh][rr - 1];  // the row a move up reaches (a walk only moves up)
+        const uint2* rp = &G.row[hh][rr - 1];  // the row a move up reaches (a walk only moves up)
         uint32_t* recs = G.rec[hh];
         uint32_t* recp = recs;                  // step k's record at recs[k] (the steps of a live walk are its records)
-        auto row_step = [&](const uint4& w4, uint32_t* rec) {
-            const uint32_t zero = LOCAL ? (w4.z >> pos) & 1u : 0u;
+        auto row_step = [&](const uint2& w2, uint32_t* rec) {
             // (NI's bit W is set when W < 32; a run to the edge of a 32-column window finds no
             // NI bit, hence the 33rd bit and the bound)
-            const uint32_t run = min((uint32_t)__builtin_ctzll((uint64_t)(w4.x >> pos) | (1ull << 32)), (uint32_t)mW - pos);
+            const uint32_t run = min((uint32_t)__builtin_ctzll((uint64_t)(w2.x >> pos) | (1ull << 32)), (uint32_t)mW - pos);
             const uint32_t p1 = pos + run;
             const uint32_t edge = p1 >= (uint32_t)mW ? 1u : 0u;
-            const uint32_t dmove = (w4.y >> (p1 & 31u)) & 1u;
-            const uint32_t go = wl & (zero ^ 1u), mv = go & (edge ^ 1u);
-            *rec = run | (dmove << 8) | (edge << 9);
-            nrec += go;
-            pos += go * run + (mv & (dmove ^ 1u));
+            const uint32_t dmove = (w2.y >> (p1 & 31u)) & 1u;
+            const uint32_t mv = wl & (edge ^ 1u);
+            *rec = run | (dmove << 8) | (edge << 9) | (p1 << 10);  // (p1: the move's column, bit W - x)
+            nrec += wl;
+            pos += wl * run + (mv & (dmove ^ 1u));
             rr -= (int)mv;
-            zdone |= wl & zero;
             wl = mv & ((uint32_t)~rr >> 31) & (pos < (uint32_t)mW ? 1u : 0u);
         };
         // Two steps per loop iteration with the row words read one step ahead
         // into alternating registers (a single one became a copy at the loop's
         // end, which waited for the read).
-        uint4 wa = rp[1], wb;
+        uint2 wa = rp[1], wb;
         while (ballot(wl != 0u)) {
             wb = rp[0];
             __builtin_amdgcn_sched_barrier(0);  // (issued here, not sunk to its use)
@@ -514,6 +520,51 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // goes with the events: ~1,000 a config-2 pair, about half of them M moves that
         // continue an M run).  Records 4 lw .. 4 lw + 3 per lane; the pair's M-move and
         // no-I-run masks over its 16 records are OR-ed over the pair's 4 lanes.
+        bool zstop = false;
+        if constexpr (LOCAL) {
+            // the cost before record k: H(k + 1) = H(k) - gap (run + a D move) - s (an M move,
+            // s of the cell it leaves: query row mr - k, column x = W - p1); the walk ends on
+            // the first record k in 1 .. nrec with H(k) = 0 (a gap move never lowers H, so only
+            // after an M move).  Records 4 lw .. 4 lw + 3 per lane, prefix over the quad.
+            int dk[4], sum = 0;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h;
+                const uint32_t rc = k < nrec ? recs[k] : 0x200u;
+                const bool ed = rc & 0x200u, dm = rc & 0x100u;
+                const uint32_t x = (uint32_t)mW - ((rc >> 10) & 63u);  // (p1 <= W: x in 0 .. 32)
+                const uint2 tv = G.tb[8u + x];
+                const uint32_t q = G.qb[hh][(uint32_t)(mr - (int)k) & 15u];
+                int sc;
+                if (tab) sc = (int)(((hh ? tv.y : tv.x) >> (8u * ((q >> 1) & 3u))) & 0xFFu) - 128 + gap;  // ck_gain_table
+                else sc = ((tv.x >> (16 * hh)) & 0xFFu) == q ? ma : mi;
+                dk[h] = -gap * (int)((rc & 63u) + (!ed && dm ? 1u : 0u)) - (!ed && !dm ? sc : 0);
+                sum += dk[h];
+            }
+            int inc = sum;
+            const int s1 = (int)quad<0x90>((uint32_t)inc);
+            inc += lw >= 1 ? s1 : 0;
+            const int s2 = (int)quad<0x40>((uint32_t)inc);
+            inc += lw >= 2 ? s2 : 0;
+            const int tot = (int)quad<0xFF>((uint32_t)inc);
+            int hk = mcost + inc - sum;  // H before record 4 lw
+            uint32_t zf = 0;
+#pragma unroll
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h;
+                zf |= (k >= 1u && k <= nrec && hk == 0) ? 1u << k : 0u;
+                hk += dk[h];
+            }
+            zf |= (lw == 3 && nrec >= 16u && hk == 0) ? 1u << 16 : 0u;  // after the 16th record
+            const uint32_t z1 = quad<0xB1>(zf);
+            zf |= z1;
+            const uint32_t z2 = quad<0x4E>(zf);
+            zf |= z2;
+            const uint32_t kz = (uint32_t)__builtin_ctz(zf | (1u << 17));
+            zstop = kz <= nrec;
+            nrec = min(nrec, kz);
+            mcost += tot;  // (stopped: no longer read)
+        }
         {
             uint32_t rcs[4], mm = 0, zm = 0;
 #pragma unroll
@@ -582,7 +633,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 kI = 0;
             }
             ++windows;
-            const bool done = zdone || mi_ < 1 || mj < 1;  // row 0 / column 0: H = 0
+            const bool done = zstop || mi_ < 1 || mj < 1;  // row 0 / column 0: H = 0
             if (!LOCAL && done) {
                 // the boundary: INSERTs along row 0, DELETEs down column 0 (:81-92) -- after an
                 // I run that reached column 0 in this window

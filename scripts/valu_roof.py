@@ -32,8 +32,12 @@ SIMDS, CLOCK = 256 * 4, 2.4e9
 KERNELS = {
     "dual_fill_kernel<1, true, true>": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1", "-DTA_DUAL_BLK"],
                                         "dual_fill_kernelILi1ELb1ELb1E"),
-    "dual_fill_ck_kernel": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1", "-DTA_DUAL_BLK", "-DTA_DUAL_CK=1"],
-                            "dual_fill_ck_kernel"),
+    "dual_fill_ck_kernel<1>": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1", "-DTA_DUAL_BLK", "-DTA_DUAL_CK=1"],
+                               "dual_fill_ck_kernelILi1E"),
+    "dual_fill_ck_kernel<0>": ("ta_dual.hip", ["-DTA_DUAL_MODE=0", "-DTA_DUAL_CIGAR=1", "-DTA_DUAL_BLK", "-DTA_DUAL_CK=1"],
+                               "dual_fill_ck_kernelILi0E"),
+    "dual_fill_ck_kernel<2>": ("ta_dual.hip", ["-DTA_DUAL_MODE=2", "-DTA_DUAL_CIGAR=1", "-DTA_DUAL_BLK", "-DTA_DUAL_CK=1"],
+                               "dual_fill_ck_kernelILi2E"),
     "dual_fill_kernel<1, true, false>": ("ta_dual.hip", ["-DTA_DUAL_MODE=1", "-DTA_DUAL_CIGAR=1"],
                                          "dual_fill_kernelILi1ELb1ELb0E"),
     "dual_fill_kernel<2, true, false>": ("ta_dual.hip", ["-DTA_DUAL_MODE=2", "-DTA_DUAL_CIGAR=1"],

@@ -1,9 +1,10 @@
 // tests/cpp/range_proofs.cpp -- brute-force check of the range bounds the
 // packed local fills rely on for their three-input max on f16 bit patterns
 // (every value must stay in [0, 0x7BFF]):
-//   * local_max3_offset (ta_layout.h, ta_dual.hip): S = 16H + z*j - i (z = 1 - 16 ma)
-//     plus the offset and the lane frame (z + 16) * lane, for every cell of every row up to n + 15 (the last lane's
-//     padding rows) and every candidate (diag / left / up before the max);
+//   * local_max3_offset (ta_layout.h, ta_dual.hip): S = 16H + z*j - i in both frames
+//     (z = 1 - 16 ma, and the equal-gain z = -1 of the fills without codes) plus the
+//     offset and the lane frame (z + 16) * lane, for every cell of every row up to n + 15
+//     (the last lane's padding rows) and every candidate (diag / left / up before the max);
 //   * flex_local_fits (ta_planner.cpp, ta_flex.hip): H itself is bounded by the
 //     planner's hmax for every cell, and every cell and candidate of the local
 //     flexible fill's frame (ta_layout.h flex_local_c0: zu - gap*r + H with the
@@ -40,16 +41,16 @@ int main(int argc, char** argv) {
         std::string q(n + 16, 'A'), t(m, 'A');
         for (auto& c : q) c = qalpha[rng() % na];
         for (auto& c : t) c = talpha[rng() % na];
-        const int off = ta::local_max3_offset(n, m, ma, mi, gap);
+        const int offs[2] = {ta::local_max3_offset(n, m, ma, mi, gap, false),
+                             ta::local_max3_offset(n, m, ma, mi, gap, true)};
         const bool flex = ta::flex_local_fits(n, m, ma, mi, gap);
-        if (off < 0 && !flex) continue;
-        dual_cases += off >= 0;
+        if (offs[0] < 0 && offs[1] < 0 && !flex) continue;
+        dual_cases += (offs[0] >= 0) + (offs[1] >= 0);
         flex_cases += flex;
         // rows up to n + 15: the padding rows compute on whatever bytes sit there
         const uint32_t N = n + 15;
         std::vector<long> H((N + 1) * (m + 1), 0);
         auto at = [&](uint32_t i, uint32_t j) -> long& { return H[(size_t)i * (m + 1) + j]; };
-        const long z = 1 - 16L * ma;
         long hmax_pl = (long)std::min(n, m) * std::max({0, ma, mi}) + ((long)n + m) * std::max(0, gap);
         for (uint32_t i = 1; i <= N; ++i)
             for (uint32_t j = 1; j <= m; ++j) {
@@ -61,16 +62,21 @@ int main(int argc, char** argv) {
                 if (u > h) h = u;
                 if (h < 0) h = 0;
                 at(i, j) = h;
-                if (off >= 0) {
+                for (int eq = 0; eq < 2; ++eq) {
+                    const int off = offs[eq];
+                    if (off < 0) continue;
                     // S of the cell and of each candidate (same row/column offset), in
                     // the frame of the lane that holds row i: + (z + 16) * lane
+                    const long z = ta::local_max3_z(ma, eq != 0);
                     const long lane = (long)(((i - 1) % 1024) / 16);
+                    // (eq: the left and up candidates enter as one max plus the shared gain --
+                    // the same values)
                     for (long cand : {d, l, u, h}) {
                         const long s = 16 * cand + z * (long)j - (long)i + off + (z + 16) * lane;
                         ++checked;
                         if (s < 0 || s > 0x7BFF) {
-                            std::printf("max3 offset violated: n=%u m=%u sc=%d,%d,%d i=%u j=%u cand=%ld S'=%ld off=%d\n",
-                                        n, m, ma, mi, gap, i, j, cand, s, off);
+                            std::printf("max3 offset violated: eq=%d n=%u m=%u sc=%d,%d,%d i=%u j=%u cand=%ld S'=%ld off=%d\n",
+                                        eq, n, m, ma, mi, gap, i, j, cand, s, off);
                             return 1;
                         }
                     }

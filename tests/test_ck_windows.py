@@ -174,12 +174,15 @@ def test_window_loads_in_bounds(n, m):
             assert 0 <= min(16 * g + 2 * lg + 1, n - 1) < n
 
 
-def kernel_events_walk(H, D, I, i, j):
+def kernel_events_walk(H, D, I, i, j, q, t, sc):
     """The kernel's walk at the bit level (traceback_ck_kernel): per window the
-    row words NI = ~I | D, D and H = 0 of W bits (column x at bit W - x), the
-    row steps with the 33-bit run bound, records, and the events of the records
-    with the I run carried across windows -- expanded into ops (walk order)."""
-    ev, kI = [], 0
+    row words NI = ~I | D and D of W bits (column x at bit W - x), the row steps
+    with the 33-bit run bound, records, the walk's cost from the records (H
+    itself is never read but at the goal: the first record whose cell has cost 0
+    ends the walk), and the events of the records with the I run carried across
+    windows -- expanded into ops (walk order)."""
+    ma, mi, gap = sc
+    ev, kI, cost = [], 0, int(H[i, j])
     while True:
         g, r = (i - 1) >> 4, (i - 1) & 15
         lane = g & 63
@@ -189,30 +192,39 @@ def kernel_events_walk(H, D, I, i, j):
         rows = {}
         for rr in range(r + 1):
             a = 16 * g + rr + 1
-            iw = dw = zw = 0
+            iw = dw = 0
             for x in range(1, W + 1):
                 b, bit = c0 + x, 1 << (W - x)
                 iw |= bit if I[a, b] else 0
                 dw |= bit if D[a, b] else 0
-                zw |= bit if H[a, b] == 0 else 0
-            rows[rr] = ((~iw | dw) & 0xFFFFFFFF, dw, zw)
-        pos, rr, wl, zdone, recs = 0, r, 1, 0, []
+            rows[rr] = ((~iw | dw) & 0xFFFFFFFF, dw)
+        pos, rr, wl, recs = 0, r, 1, []
         while wl:
-            ni, dw, zw = rows[rr]
-            zero = (zw >> pos) & 1
+            # (past a cell with H = 0 the walk goes on over whatever codes are there; the
+            # records it lists after that are cut below)
+            ni, dw = rows[rr] if rr in rows else (0, 0)
             v = (ni >> pos) | (1 << 32)
             run = min((v & -v).bit_length() - 1, W - pos)
             p1 = pos + run
             edge = 1 if p1 >= W else 0
             dmove = (dw >> (p1 & 31)) & 1
-            go = wl & (zero ^ 1)
-            mv = go & (edge ^ 1)
-            if go:
-                recs.append(run | (dmove << 8) | (edge << 9))
-            pos += go * run + (mv & (dmove ^ 1))
+            mv = wl & (edge ^ 1)
+            recs.append(run | (dmove << 8) | (edge << 9) | (p1 << 10))
+            pos += run + (mv & (dmove ^ 1))
             rr -= mv
-            zdone |= wl & zero
             wl = mv & (1 if rr >= 0 else 0) & (1 if pos < W else 0)
+        # the cost before each record; the first record k >= 1 (k = len: after the last)
+        # with cost 0 ends the walk
+        hk, zstop = [cost], False
+        for k, rc in enumerate(recs):
+            ed, dm, x = rc & 0x200, rc & 0x100, W - ((rc >> 10) & 63)
+            s = (ma if q[16 * g + r - k] == t[c0 + x - 1] else mi) if not ed and not dm else 0
+            hk.append(hk[-1] - gap * ((rc & 63) + (1 if not ed and dm else 0)) - s)
+        for k in range(1, len(recs) + 1):
+            if hk[k] == 0:
+                recs, zstop = recs[:k], True
+                break
+        cost = hk[len(recs)]
         # M moves with no I run between them: one event at the run's last record
         mm = zm = 0
         for k, rc in enumerate(recs):
@@ -235,7 +247,7 @@ def kernel_events_walk(H, D, I, i, j):
             last = recs[-1]
             kI = ((last & 63) + (kI if len(recs) == 1 else 0)) if last & 0x200 else 0
         i, j = 16 * g + rr + 1, c0 + W - pos
-        if zdone or i < 1 or j < 1:
+        if zstop or i < 1 or j < 1:
             break
     ops = []
     for v in ev:
@@ -261,4 +273,4 @@ def test_kernel_events_walk_matches_reference(sc):
         H, D, I, gi, gj = dp(q, t, *sc)
         if H[gi, gj] <= 0:
             continue
-        assert kernel_events_walk(H, D, I, gi, gj) == reference_walk(H, D, I, gi, gj), (sc, k)
+        assert kernel_events_walk(H, D, I, gi, gj, q, t, sc) == reference_walk(H, D, I, gi, gj), (sc, k)
