@@ -61,8 +61,8 @@ sys.path.insert(0, ROOT)
 # count share queues -- two streams on one queue run one after the other.  Set
 # before anything initialises HIP.
 _HWQ = int(os.environ.get("TA_BENCH_HW_QUEUES", "16"))  # (experiments: another count)
-_HWQ_ORIG = os.environ.get("GPU_MAX_HW_QUEUES")  # (the drop-in runs keep the process default: more
-# queues cost the single-pair server's 5x9 round trip 13 -> 19 us)
+_HWQ_ORIG = os.environ.get("GPU_MAX_HW_QUEUES")  # (the drop-in runs keep the process default, 4 on
+# the box, as a plain library user does; 16 measured the same, r06h)
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < _HWQ or "TA_BENCH_HW_QUEUES" in os.environ:
     os.environ["GPU_MAX_HW_QUEUES"] = str(min(_HWQ, 32))
 
@@ -1089,9 +1089,14 @@ def main_dropin(args):
     # amd: the drop-in as shipped (pairs up to 4096 x 16384 on the resident single-pair server), run as
     # a plain library user runs it -- the process default of hardware queues, 4 on the box;
     # amd_batch_path: the same library with TEAM_ALIGN_SERVER=0 (concurrent calls combined into batches);
-    # amd_queues16: one thread under GPU_MAX_HW_QUEUES=16 (what bench.py sets for its pipelines),
-    # the r05 cause of the slower 5x9 round trip
+    # amd_queues16: one thread under GPU_MAX_HW_QUEUES=16 (what bench.py sets for its pipelines).
+    # Before the timed runs, 2 s of 1 kb calls from 16 threads: a fresh box's idle GPU runs a
+    # latency-bound 5x9 round trip at 19 us, one that has been busy at 13 (r06h: the same run's
+    # later variants, and the queue count made no difference)
     amd = os.path.join(ROOT, "build", "dropin_amd")
+    if os.path.exists(amd):
+        subprocess.run([amd, "16", "2.0", "1000x1000", str(MODES[args.mode or "local"])], capture_output=True,
+                       timeout=300, check=True, env=_dropin_env({}))
     for name, exe, env, threads in (("amd", amd, {}, (1, 8, 16)),
                                     ("amd_batch_path", amd, {"TEAM_ALIGN_SERVER": "0"}, (1, 8, 16)),
                                     ("amd_queues16", amd, {"GPU_MAX_HW_QUEUES": "16"}, (1,)),

@@ -19,34 +19,32 @@
 // checkpoint column (left), stripe g - 1's stored bottom row over c0 .. j
 // (top), the target and query bytes.
 //
-// Geometry: 4 lanes per two pairs (a quad), 32 pairs per wave.  Lane lg of a
-// group holds rows 4 lg .. 4 lg + 3 of its stripe for BOTH pairs of the group,
-// packed in int16 halves (pair A low, pair B high).  The lanes sweep the
-// window's anti-diagonals -- lane lg computes column x = k - lg + 1 at step k,
-// W + 3 steps -- the first row's up value from the lane above by DPP
-// row_shr:1 (the group's first lane: the top row), each next row's from the one
-// above it.  Local values are H + gap + B with B = mag + 1, so every value and
-// candidate is a non-negative int16 below 0x7BFF (H <= 2047 in a dual plan,
-// ta_planner.cpp fits_int16): the clamp and both maxima are one
-// v_pk_maximum3_f16 (ta_packed.h pk_max3_pos).  Each step's D and I signs of
-// the four rows and both pairs go into byte accumulators per 8 steps
+// Geometry (r06): 8 lanes per two pairs, 16 pairs per wave.  Lane lg of a group
+// holds rows 2 lg and 2 lg + 1 of its stripe for BOTH pairs of the group, packed
+// in int16 halves (pair A low, pair B high).  The lanes sweep the window's
+// anti-diagonals -- lane lg computes column x = k - lg + 1 at step k, W + 7
+// steps -- the first row's up value from the lane above by DPP row_shr:1 (the
+// group's first lane: the top row), the second row's from the first.  Values
+// are H + gap + B with B = mag + 1, so every value and candidate is a
+// non-negative int16 below 0x7BFF (H <= 2047 in a dual plan, ta_planner.cpp
+// fits_int16): the clamp and both maxima are one v_pk_maximum3_f16
+// (ta_packed.h pk_max3_pos).  Each step's D, I and H = 0 signs of both rows and
+// both pairs (12 bits) go into three byte accumulators per 8 steps
 // (sign_bytes + one bit insert, as the dual fill's codes).  Per pair and row
-// two 32-bit words then go to LDS (column x at bit W - x): NI (cells whose move
-// is NOT I-only) and D.  The walk crosses the window one row per step (lanes
-// 0-1 of a group: its first pair, 2-3: its second): the run of I moves up to
-// the first NI bit, then the D or M move up; it leaves through the top (stripe
-// g - 1, same column) or, when the I run reaches c0, through the left edge (the
-// same stripe, the next checkpoint left).  Each row step lists a record; a
-// local walk's cost along its records finds the first cell with H = 0, where it
-// stops; the window's events for format_runs_kernel (D run above bit 16, count
-// of the move in bits 15:2, move in bits 1:0) are made from the records by the
-// pair's 2 lanes.
+// three 32-bit words then go to LDS (column x at bit W - x): NI (cells whose
+// move is NOT I-only), D, and H = 0.  The walk crosses the window one row per
+// step (lanes 0-3 of a group: its first pair, 4-7: its second): stop on a
+// cell with H = 0, else the run of I moves up to the first NI bit, then the D
+// or M move up; it leaves through the top (stripe g - 1, same column) or, when
+// the I run reaches c0, through the left edge (the same stripe, the next
+// checkpoint left).  Each row step lists a record; the window's events for
+// format_runs_kernel (D run above bit 16, count of the move in bits 15:2, move
+// in bits 1:0) are made from the records by the pair's 4 lanes.
 //
 // r05's kernel (16 lanes per two pairs, one row each, 8 pairs per wave) swept
-// a fixed 48 steps for 32 cells per lane; r06's first (8 lanes, two rows each,
-// 16 pairs per wave) W + 7 steps for 64; here W + 3 steps cover 128 cells per
-// lane, and the walk's row steps and window loads serve 32 pairs per
-// instruction.
+// a fixed 48 steps for 32 cells per lane; here 40 steps cover 64 cells per lane,
+// and the walk's row steps and window loads serve 16 pairs per instruction
+// instead of 8.
 #include "ta_device.h"
 #include "ta_packed.h"
 
@@ -55,38 +53,24 @@ namespace {
 
 constexpr int kCkLead = 17;            // columns a window reaches left of the walk's column, at least
 constexpr int kCkMaxW = kCkLead + 15;  // the widest window (checkpoints 16 columns apart)
-constexpr int kCkRows = 4;                 // rows per lane
-constexpr int kCkLanes = 16 / kCkRows;     // lanes per group (two pairs): a quad
+constexpr int kCkLanes = 8;            // lanes per group (two pairs, two rows per lane)
 constexpr int kCkGroups = kWave / kCkLanes;
-constexpr int kCkRecs = 16 / (kCkLanes / 2);  // records per walker lane (two lanes per pair)
-static_assert(kCkLanes == 4, "the walker lanes' cross-lane moves are quad_perm DPPs");
 constexpr int kCkBlocks = 5;           // sweep blocks of 8 steps
 static_assert(kCkMaxW + kCkLanes - 1 <= 8 * kCkBlocks, "a window's sweep fits the blocks");
 static_assert(8 * kCkBlocks <= 40, "a row's steps fit 40 bits (one byte + one dword)");
 
-// (LDS: 64 groups a block in <= 40 KB, i.e. four blocks a CU -- the compiler holds a kernel to
-// 128 VGPRs only when its LDS allows that occupancy)
 struct CkGroup {
-    uint16_t tbyte[kCkMaxW + 2];          // local: per x, both pairs' target bytes (A: bits 7:0)
-    uint8_t qb[2][16];                    // local: per pair, the query bytes of the stripe's rows
-    union {
-        struct {  // the sweep's operands
-            // per x (at 4 + x): both pairs' gain tables of the target byte (TAB windows: .x
-            // pair A's, .y pair B's, ck_gain_table), else their target bytes (.x bits 7:0,
-            // 23:16); x <= 32 (the sweep's steps past W read what follows: columns past W)
-            uint2 tb[4 + kCkMaxW + 1];
-            uint32_t top[8 * kCkBlocks + 1];  // per x: both pairs' H(16g, c0 + x) + gap + B (int16 halves)
-        } s;
-        struct {  // the walk's
-            uint16_t rec[2][16];  // per pair: the window's row steps
-            // (the walk reads the rows above row 0 -- up to 18 -- of walkers that already
-            // left, from inside the group)
-            uint2 row[2][16];     // per pair and row: NI, D window words
-        } w;
-    } u;
+    uint32_t top[8 * kCkBlocks + 1];     // per x: both pairs' H(16g, c0 + x) + gap + B (int16 halves)
+    // per x (at 8 + x): both pairs' gain tables of the target byte (TAB windows: .x pair
+    // A's, .y pair B's, ckGainTable), else their target bytes (.x bits 7:0, 23:16)
+    uint2 tb[8 + 8 * kCkBlocks + 1];
+    // (after top / tb: the walk reads the row above row 0 -- up to 18 rows -- of
+    // walkers that already left, from inside the group)
+    uint2 row[2][16];                    // per pair and row: NI, D window words
+    uint32_t rec[2][16];                 // per pair: the window's row steps
+    uint8_t qb[2][16];                   // local: per pair, the query bytes of the stripe's rows
 };
-static_assert(offsetof(CkGroup, u) + offsetof(decltype(CkGroup::u), w.row) >= 18 * sizeof(uint2), "room above a walker's row 0");
-static_assert(64 * sizeof(CkGroup) + 1024 <= 40 * 1024, "four blocks a CU");
+static_assert(offsetof(CkGroup, row) >= 18 * sizeof(uint2), "room above a walker's row 0");
 
 // TAB windows (every query row of both pairs is A, C, G or T; ta_packed.h
 // mismatch_table): the diagonal gain of a cell is a byte of its column's gain
@@ -145,8 +129,7 @@ struct CkPair {
 };
 
 // (<= 128 VGPRs: beside the next batch's fill -- 96 VGPRs a wave -- a walk wave then displaces
-// one fill wave of its SIMD, not two; CkGroup keeps the LDS to the four blocks a CU that
-// occupancy needs)
+// one fill wave of its SIMD, not two)
 template <int MODE>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) void traceback_ck_kernel(TraceArgs a) {
     constexpr bool LOCAL = MODE == kLocal;
@@ -155,8 +138,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     // a latency-bound chain: beside the next batch's fill (align.DevicePipeline)
     // its instructions go first at the SIMD's issue arbiter (measured neutral)
     __builtin_amdgcn_s_setprio(3);
-    const int lane = (int)threadIdx.x & 63, lg = lane & (kCkLanes - 1), hh = lg >> 1, lw = lg & 1;
-    CkGroup& G = groups[threadIdx.x / kCkLanes];
+    const int lane = (int)threadIdx.x & 63, lg = lane & 7, hh = lg >> 2, lw = lg & 3;
+    CkGroup& G = groups[threadIdx.x >> 3];
     const int ma = a.match, mi = a.mismatch, gap = a.gap;
     const int mag = max(max(max(ma, -ma), max(mi, -mi)), max(max(gap, -gap), 1));
     const int B = mag + 1;   // bias: values H + gap + B >= 1
@@ -172,7 +155,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
         CkPair& c = S[h];
-        const uint32_t slot = ((blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kCkGroups + (uint32_t)(lane / kCkLanes)) * 2 + h;
+        const uint32_t slot = ((blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kCkGroups + (uint32_t)(lane >> 3)) * 2 + h;
         c.has = slot < a.count;
         c.p = c.has ? (a.order ? a.order[a.begin + slot] : a.begin + slot) : 0u;
         if (c.has && a.pflag && a.pflag[c.p]) c.has = false;  // '-' bytes: the fallback walk
@@ -201,7 +184,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         live[h] = c.has && H > 0;  // a positive score has its goal at i, j >= 1
         hc[h] = H;
     }
-    // the walker's own pair (lanes 0-1: pair A, 2-3: pair B)
+    // the walker's own pair (lanes 0-3: pair A, 4-7: pair B)
     const bool mhas = hh ? S[1].has : S[0].has;
     const uint32_t mp = hh ? S[1].p : S[0].p, mnm = hh ? S[1].n + S[1].m : S[0].n + S[0].m;
     uint32_t* const rout = a.runs + (mhas ? band_runs_off(a.slot_off[mp]) : 0);
@@ -247,19 +230,14 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
     __syncthreads();
     uint32_t KN = swar_k(-128);
     asm volatile("" : "+s"(KN));
-    uint32_t acc[kCkRows][kCkBlocks];
+    uint32_t acc[2][kCkBlocks];
 #pragma unroll
-    for (int b = 0; b < kCkBlocks; ++b)
-#pragma unroll
-        for (int r = 0; r < kCkRows; ++r) acc[r][b] = 0u;
+    for (int b = 0; b < kCkBlocks; ++b) acc[0][b] = acc[1][b] = 0u;
 
     while (ballot(live[0] || live[1])) {
         // ---- both pairs' windows: loads first (one wait for all), then the decodes
-        // (top: columns x = lg + 4q, q < 9 -- the rest lie past every W; targets: x = 1 + lg + 4q)
-        constexpr int kTopQ = (kCkMaxW + kCkLanes) / kCkLanes, kTopW = (8 * kCkBlocks + kCkLanes) / kCkLanes;
-        constexpr int kTbQ = kCkMaxW / kCkLanes;
         int g[2], r[2], c0[2], W[2];
-        uint32_t vl[2][2], vt[2][kTopQ], vb[2][kTbQ], vq[2][kCkRows];
+        uint32_t vl[2], vt[2][5], vb[2][4], vq[2][2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const CkPair& c = S[h];
@@ -271,45 +249,42 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             // before the stripe's first column (16 (b + 1) - l <= 0: j <= 32 then)
             c0[h] = e >= 16 ? max((e >> 4) * 16 - l, 0) : 0;
             W[h] = live[h] ? cj[h] - c0[h] : 0;
-            // left: rows 4 lg .. 4 lg + 3 of checkpoint column c0 (four adjacent int16, two dwords)
+            // left: rows 2 lg, 2 lg + 1 of checkpoint column c0 (two adjacent int16, one dword)
             const bool hl = live[h] && c0[h] > 0;
             const uint32_t li = hl ? (uint32_t)ck_col_index((uint32_t)g[h] >> 6, (uint32_t)(e >> 4) - 1u, (uint32_t)l, c.nb,
-                                                            (uint32_t)(kCkRows * lg)) : 0u;
-            vl[h][0] = *reinterpret_cast<const uint32_t*>(c.P + li);
-            vl[h][1] = *reinterpret_cast<const uint32_t*>(c.P + li + 2);
-            // top: stripe g - 1's bottom row at columns c0 + x, x = lg + 4q <= W (its step
-            // c0 + x + lu - 1); stripe 0 reads a dummy (its top row is row 0: H = 0)
+                                                            2u * (uint32_t)lg) : 0u;
+            vl[h] = *reinterpret_cast<const uint32_t*>(c.P + li);
+            // top: stripe g - 1's bottom row at columns c0 + x, x = lg + 8q (its step c0 + x + lu - 1);
+            // stripe 0 reads a dummy (its top row is row 0: H = 0)
             // (ck_row_index in int: step t0 is -1 for column 0 of lane 0 when lu = 0 -- a value
             // masked below, loaded from index 0 instead -- and then block -1 + 1 is step 15's)
             const bool ht = live[h] && g[h] > 0;
             const int gu = ht ? g[h] - 1 : 0, lu = gu & 63, pu = gu >> 6;
-            const int t0 = ht ? c0[h] + lg + lu - 1 : 0;
+            const int t0 = ht ? c0[h] + lg + lu - 1 : 0, t1 = t0 + 8;
             const int base = ht ? pu * (int)c.nb * 2048 + lu * 16 : 0;
-            int ib[4];  // steps t0 + 4b; + 16 steps: the next block, same step within it (+ 1024)
+            const int i0 = base + (t0 >> 4) * 1024 + (t0 & 15), i1 = base + (t1 >> 4) * 1024 + (t1 & 15);
+            vt[h][0] = c.P[max(i0, 0)];
+            vt[h][1] = c.P[i1];
+            vt[h][2] = c.P[i0 + 1024];  // (16 columns on: the next block, same step within it)
+            vt[h][3] = c.P[i1 + 1024];
+            vt[h][4] = c.P[i0 + 2048];
+            // target bytes of columns x = 1 + lg + 8q (only x <= W: the last pair's bytes end the buffer)
 #pragma unroll
-            for (int b = 0; b < 4; ++b) ib[b] = base + ((t0 + 4 * b) >> 4) * 1024 + ((t0 + 4 * b) & 15);
-#pragma unroll
-            for (int q = 0; q < kTopQ; ++q) {
-                const int x = lg + kCkLanes * q;
-                vt[h][q] = c.P[x <= W[h] ? max(ib[q & 3] + 1024 * (q >> 2), 0) : 0];
-            }
-            // target bytes of columns x = 1 + lg + 4q (only x <= W: the last pair's bytes end the buffer)
-#pragma unroll
-            for (int q = 0; q < kTbQ; ++q) {
-                const int x = 1 + lg + kCkLanes * q;
+            for (int q = 0; q < 4; ++q) {
+                const int x = 1 + lg + 8 * q;
                 vb[h][q] = x <= W[h] ? (uint32_t)c.T[c0[h] + x - 1] : 0u;
             }
             // query bytes of the lane's rows (rows past n: any byte, below the walk; pairs
             // not walking: 'A', which keeps a TAB window)
-            const uint32_t ir = 16u * (uint32_t)g[h] + (uint32_t)(kCkRows * lg);  // the first row - 1
+            const uint32_t ir = 16u * (uint32_t)g[h] + 2u * (uint32_t)lg;  // the first row - 1
             const uint32_t qn = c.n ? c.n - 1u : 0u;
-#pragma unroll
-            for (int rw = 0; rw < kCkRows; ++rw) vq[h][rw] = live[h] ? c.Q[min(ir + (uint32_t)rw, qn)] : 0x41u;
+            vq[h][0] = live[h] ? c.Q[min(ir, qn)] : 0x41u;
+            vq[h][1] = live[h] ? c.Q[min(ir + 1u, qn)] : 0x41u;
         }
         // decodes (ta_layout.h ck_decode, plus gap + B): v = (s - off - z j + i - dl l) / 16 + gap + B
         // is exact in 16-bit wrap-around arithmetic ((s + C) mod 2^16 = 16 (H + gap + B) < 2^16),
         // so both pairs decode together: one packed add of C and one packed shift
-        uint32_t gl[kCkRows], qs[kCkRows], mT = 0, mL[kCkRows] = {};
+        uint32_t gl0, gl1, q0, q1, mT = 0, mL0 = 0, mL1 = 0;
         bool acgt = true;
         {
             int CL[2], CT[2];
@@ -317,102 +292,80 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             for (int h = 0; h < 2; ++h) {
                 const CkPair& c = S[h];
                 const int l = g[h] & 63, lu = (g[h] - 1) & 63;
-                const int ir = 16 * g[h] + kCkRows * lg + 1;  // the lane's first row
+                const int ir = 16 * g[h] + 2 * lg + 1;  // the lane's first row
                 CL[h] = 16 * GB - c.off - c.z * c0[h] + ir - c.dl * l;
                 CT[h] = 16 * GB - c.off - c.z * (c0[h] + lg) + 16 * g[h] - c.dl * lu;
                 // (rows past n: H = 0 too, see ck_gain_table)
                 const bool hl = live[h] && c0[h] > 0;
-#pragma unroll
-                for (int rw = 0; rw < kCkRows; ++rw) {
-                    mL[rw] |= (hl && ir + rw <= (int)c.n) ? 0xFFFFu << (16 * h) : 0u;
-                    acgt = acgt && is_acgt(vq[h][rw]);
-                }
+                mL0 |= (hl && ir <= (int)c.n) ? 0xFFFFu << (16 * h) : 0u;
+                mL1 |= (hl && ir + 1 <= (int)c.n) ? 0xFFFFu << (16 * h) : 0u;
                 mT |= (live[h] && g[h] > 0) ? 0xFFFFu << (16 * h) : 0u;
+                acgt = acgt && is_acgt(vq[h][0]) && is_acgt(vq[h][1]);
             }
             const uint32_t cl = ((uint32_t)CL[0] & 0xFFFFu) | ((uint32_t)CL[1] << 16);
             const uint32_t ct = ((uint32_t)CT[0] & 0xFFFFu) | ((uint32_t)CT[1] << 16);
-            uint32_t lv[kCkRows];  // rows 4 lg + rw of A, B
-#pragma unroll
-            for (int rw = 0; rw < kCkRows; ++rw)
-                lv[rw] = __builtin_amdgcn_perm(vl[1][rw >> 1], vl[0][rw >> 1], (rw & 1) ? 0x07060302u : 0x05040100u);
+            const uint32_t l0 = __builtin_amdgcn_perm(vl[1], vl[0], 0x05040100u);  // row 2 lg of A, B
+            const uint32_t l1 = __builtin_amdgcn_perm(vl[1], vl[0], 0x07060302u);  // row 2 lg + 1
             // column 0 (c0 = 0, x = 0): the boundary
             const uint32_t m0 = mT & (lg == 0 ? ((c0[0] > 0 ? 0xFFFFu : 0u) | (c0[1] > 0 ? 0xFFFF0000u : 0u)) : ~0u);
             if constexpr (LOCAL) {
-                uint32_t cr = cl;
-#pragma unroll
-                for (int rw = 0; rw < kCkRows; ++rw) {
-                    gl[rw] = vsel(mL[rw], pk_lshr4(pk_add(lv[rw], cr)), GB2);
-                    cr = pk_add(cr, ONE);
-                }
+                gl0 = vsel(mL0, pk_lshr4(pk_add(l0, cl)), GB2);
+                gl1 = vsel(mL1, pk_lshr4(pk_add(l1, pk_add(cl, ONE))), GB2);
                 // the decode constant moves by -z per column
-                const uint32_t dx = ((uint32_t)(-kCkLanes * S[0].z) & 0xFFFFu) | ((uint32_t)(-kCkLanes * S[1].z) << 16);
+                const uint32_t dx = ((uint32_t)(-8 * S[0].z) & 0xFFFFu) | ((uint32_t)(-8 * S[1].z) << 16);
                 uint32_t ctq = ct;
 #pragma unroll
-                for (int q = 0; q < kTopW; ++q) {
+                for (int q = 0; q < 5; ++q) {
                     // (columns past W: H = 0, see ck_gain_table)
-                    const int x = lg + kCkLanes * q;
+                    const int x = lg + 8 * q;
                     const uint32_t mw = (x <= W[0] ? 0xFFFFu : 0u) | (x <= W[1] ? 0xFFFF0000u : 0u);
-                    if (q < kTopQ) {
-                        const uint32_t s = vt[0][q < kTopQ ? q : 0] | (vt[1][q < kTopQ ? q : 0] << 16);
-                        G.u.s.top[x] = vsel((q == 0 ? m0 : mT) & mw, pk_lshr4(pk_add(s, ctq)), GB2);
-                    } else if (x <= 8 * kCkBlocks) {
-                        G.u.s.top[x] = GB2;
-                    }
+                    const uint32_t s = vt[0][q] | (vt[1][q] << 16);
+                    G.top[x] = vsel((q == 0 ? m0 : mT) & mw, pk_lshr4(pk_add(s, ctq)), GB2);
                     ctq = pk_add(ctq, dx);
                 }
             } else {
                 // the stored S values as they are; the boundaries computed: column 0 S(i, 0) =
                 // C0 i, row 0 S(0, j) = R0 j (stripe 0's top row)
-                const int ir0 = 16 * g[0] + kCkRows * lg + 1, ir1 = 16 * g[1] + kCkRows * lg + 1;
+                const int ir0 = 16 * g[0] + 2 * lg + 1, ir1 = 16 * g[1] + 2 * lg + 1;
                 const uint32_t cb = ((uint32_t)(C0 * ir0) & 0xFFFFu) | ((uint32_t)(C0 * ir1) << 16);
                 const uint32_t mE = (live[0] && c0[0] > 0 ? 0xFFFFu : 0u) | (live[1] && c0[1] > 0 ? 0xFFFF0000u : 0u);
-                uint32_t cr = cb;
-#pragma unroll
-                for (int rw = 0; rw < kCkRows; ++rw) {
-                    gl[rw] = vsel(mE, lv[rw], cr);
-                    cr = pk_add(cr, rep16(C0));
-                }
+                gl0 = vsel(mE, l0, cb);
+                gl1 = vsel(mE, l1, pk_add(cb, rep16(C0)));
                 const uint32_t rowb = ((uint32_t)(R0 * (c0[0] + lg)) & 0xFFFFu) | ((uint32_t)(R0 * (c0[1] + lg)) << 16);
                 const uint32_t colb = ((uint32_t)(C0 * 16 * g[0]) & 0xFFFFu) | ((uint32_t)(C0 * 16 * g[1]) << 16);
                 uint32_t rq = rowb;
 #pragma unroll
-                for (int q = 0; q < kTopW; ++q) {
-                    // (past every W the values are never read as cells of the walk)
-                    const int x = lg + kCkLanes * q;
-                    const uint32_t s = q < kTopQ ? (vt[0][q < kTopQ ? q : 0] | (vt[1][q < kTopQ ? q : 0] << 16)) : rq;
+                for (int q = 0; q < 5; ++q) {
+                    const uint32_t s = vt[0][q] | (vt[1][q] << 16);
                     const uint32_t alt = q == 0 ? vsel(mT, colb, rq) : rq;  // (q > 0: column > 0)
-                    if (x <= 8 * kCkBlocks) G.u.s.top[x] = vsel(q == 0 ? m0 : mT, s, alt);
-                    rq = pk_add(rq, rep16(kCkLanes * R0));
+                    G.top[lg + 8 * q] = vsel(q == 0 ? m0 : mT, s, alt);
+                    rq = pk_add(rq, rep16(8 * R0));
                 }
             }
         }
         if constexpr (LOCAL) {
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
-                *reinterpret_cast<uint32_t*>(&G.qb[h][kCkRows * lg]) = vq[h][0] | (vq[h][1] << 8) | (vq[h][2] << 16) | (vq[h][3] << 24);
-#pragma unroll
-            for (int q = 0; q < kTbQ; ++q) G.tbyte[1 + lg + kCkLanes * q] = (uint16_t)(vb[0][q] | (vb[1][q] << 8));
+            for (int h = 0; h < 2; ++h) *reinterpret_cast<uint16_t*>(&G.qb[h][2 * lg]) = (uint16_t)(vq[h][0] | (vq[h][1] << 8));
         }
-        static_assert(kCkRows == 4, "one dword of query bytes per lane and pair");
         // the window's sweep kind (wave-uniform): TAB when every query row is A, C, G, T
         const bool tab = tab_ok && !ballot(!acgt);
         if (tab) {
 #pragma unroll
-            for (int q = 0; q < kTbQ; ++q) G.u.s.tb[5 + lg + kCkLanes * q] = make_uint2(gtab[vb[0][q]], gtab[vb[1][q]]);
-#pragma unroll
-            for (int rw = 0; rw < kCkRows; ++rw) qs[rw] = row_selector(vq[0][rw], vq[1][rw]);
+            for (int q = 0; q < 4; ++q) G.tb[9 + lg + 8 * q] = make_uint2(gtab[vb[0][q]], gtab[vb[1][q]]);
+            q0 = row_selector(vq[0][0], vq[1][0]);
+            q1 = row_selector(vq[0][1], vq[1][1]);
         } else {
 #pragma unroll
-            for (int q = 0; q < kTbQ; ++q) G.u.s.tb[5 + lg + kCkLanes * q] = make_uint2(vb[0][q] | (vb[1][q] << 16), 0u);
-#pragma unroll
-            for (int rw = 0; rw < kCkRows; ++rw) qs[rw] = vq[0][rw] | (vq[1][rw] << 16);
+            for (int q = 0; q < 4; ++q) G.tb[9 + lg + 8 * q] = make_uint2(vb[0][q] | (vb[1][q] << 16), 0u);
+            q0 = vq[0][0] | (vq[1][0] << 16);
+            q1 = vq[0][1] | (vq[1][1] << 16);
         }
         ck_wave_sync();
 
-        // ---- the sweep: step k, lane lg computes column x = k - lg + 1 of its four rows of both pairs
+        // ---- the sweep: step k, lane lg computes column x = k - lg + 1 of its two rows of both pairs
         const int need = max(W[0], W[1]) + kCkLanes - 1;  // steps this lane's pairs need
-        uint32_t upp = G.u.s.top[0];  // the previous step's up candidate of row 4 lg (lane 0: H(16g, c0) + gap + B)
-        const uint2* tbl = &G.u.s.tb[5 - lg];
+        uint32_t upp = G.top[0];  // the previous step's up candidate of row 2 lg (lane 0: H(16g, c0) + gap + B)
+        const uint2* tbl = &G.tb[9 - lg];
         auto block = [&](auto kb_tag, auto tab_tag) {
             constexpr int kb = decltype(kb_tag)::value;
             constexpr bool TAB = decltype(tab_tag)::value;
@@ -420,53 +373,67 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             uint2 bv[8];
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-                tv[s] = G.u.s.top[kb + s + 1];
+                tv[s] = G.top[kb + s + 1];
                 if constexpr (TAB) bv[s] = tbl[kb + s];
                 else bv[s].x = tbl[kb + s].x;
             }
-            uint32_t ac[kCkRows];
+            uint32_t a0 = acc[0][kb / 8], a1 = acc[1][kb / 8];
+            if constexpr (!LOCAL) {
+                // global / semi: S values, no clamp; D and I signs of saturating differences
+                // (S and its candidates are int16 -- fits_int16 -- their differences need not be)
 #pragma unroll
-            for (int rw = 0; rw < kCkRows; ++rw) ac[rw] = acc[rw][kb / 8];
+                for (int s = 0; s < 8; ++s) {
+                    const uint32_t dpp = (uint32_t)__builtin_amdgcn_mov_dpp((int)gl1, 0x111, 0xF, 0xF, true);
+                    const uint32_t up0 = first ? tv[s] : dpp;
+                    const uint32_t e0 = TAB ? mismatch_flags(bv[s].x, bv[s].y, q0) : pk_min_u16(q0 ^ bv[s].x, ONE);
+                    const uint32_t e1 = TAB ? mismatch_flags(bv[s].x, bv[s].y, q1) : pk_min_u16(q1 ^ bv[s].x, ONE);
+                    const uint32_t dg0 = pk_mad_i16(e0, KE2, upp), lf0 = pk_add(gl0, GL2);
+                    const uint32_t m10 = pk_max(dg0, lf0), hn0 = pk_max(m10, up0);
+                    const uint32_t dg1 = pk_mad_i16(e1, KE2, gl0), lf1 = pk_add(gl1, GL2);
+                    const uint32_t m11 = pk_max(dg1, lf1), hn1 = pk_max(m11, hn0);
+                    const uint32_t mk = 0x01010101u << (7 - s);
+                    a0 = bfi(mk, sign_bytes(pk_sub_sat(m10, up0), pk_sub_sat(dg0, lf0)), a0);  // [I0A, I0B, D0A, D0B]
+                    a1 = bfi(mk, sign_bytes(pk_sub_sat(m11, hn0), pk_sub_sat(dg1, lf1)), a1);  // [I1A, I1B, D1A, D1B]
+                    if (kb >= 8 || kb + s >= lg) {
+                        gl0 = hn0;
+                        gl1 = hn1;
+                    }
+                    upp = up0;
+                }
+                acc[0][kb / 8] = a0;
+                acc[1][kb / 8] = a1;
+                return;
+            }
 #pragma unroll
             for (int s = 0; s < 8; ++s) {
-                // the first row: up from the lane above's last row (row_shr:1; a group's
-                // first lane: the top row), diagonal = the previous step's up; each next row:
-                // up = the row above's new value, diagonal = its previous one
-                const uint32_t dpp = (uint32_t)__builtin_amdgcn_mov_dpp((int)gl[kCkRows - 1], 0x111, 0xF, 0xF, true);
+                // the first row: up from the lane above's second row (row_shr:1; a
+                // group's first lane: the top row), diagonal = the previous step's up
+                const uint32_t dpp = (uint32_t)__builtin_amdgcn_mov_dpp((int)gl1, 0x111, 0xF, 0xF, true);
                 const uint32_t up0 = first ? tv[s] : dpp;
+                uint32_t dg0, dg1;
+                if constexpr (TAB) dg0 = upp + mismatch_flags(bv[s].x, bv[s].y, q0) + KN;  // (v_add3_u32)
+                else dg0 = pk_mad_i16(pk_min_u16(q0 ^ bv[s].x, ONE), KD2, pk_add(upp, SA2));
+                const uint32_t m10 = pk_max(dg0, gl0);
+                const uint32_t hn0 = pk_max3_pos(m10, up0, B2);  // H + B (clamp at H = 0)
+                const uint32_t gn0 = pk_add(hn0, GAP2);
+                // the second row: up = the first row's new value, diagonal = its previous one
+                if constexpr (TAB) dg1 = gl0 + mismatch_flags(bv[s].x, bv[s].y, q1) + KN;
+                else dg1 = pk_mad_i16(pk_min_u16(q1 ^ bv[s].x, ONE), KD2, pk_add(gl0, SA2));
+                const uint32_t m11 = pk_max(dg1, gl1);
+                const uint32_t hn1 = pk_max3_pos(m11, gn0, B2);
+                const uint32_t gn1 = pk_add(hn1, GAP2);
+                // signs: D (up beats both), I (left beats the diagonal)
                 const uint32_t mk = 0x01010101u << (7 - s);
-                uint32_t up = up0, dv = upp, gn[kCkRows];
-#pragma unroll
-                for (int rw = 0; rw < kCkRows; ++rw) {
-                    if constexpr (!LOCAL) {
-                        // global / semi: S values, no clamp; D and I signs of saturating differences
-                        // (S and its candidates are int16 -- fits_int16 -- their differences need not be)
-                        const uint32_t e = TAB ? mismatch_flags(bv[s].x, bv[s].y, qs[rw]) : pk_min_u16(qs[rw] ^ bv[s].x, ONE);
-                        const uint32_t dg = pk_mad_i16(e, KE2, dv), lf = pk_add(gl[rw], GL2);
-                        const uint32_t m1 = pk_max(dg, lf), hn = pk_max(m1, up);
-                        ac[rw] = bfi(mk, sign_bytes(pk_sub_sat(m1, up), pk_sub_sat(dg, lf)), ac[rw]);  // [I A, I B, D A, D B]
-                        gn[rw] = hn;
-                    } else {
-                        uint32_t dg;
-                        if constexpr (TAB) dg = dv + mismatch_flags(bv[s].x, bv[s].y, qs[rw]) + KN;  // (v_add3_u32)
-                        else dg = pk_mad_i16(pk_min_u16(qs[rw] ^ bv[s].x, ONE), KD2, pk_add(dv, SA2));
-                        const uint32_t m1 = pk_max(dg, gl[rw]);
-                        const uint32_t hn = pk_max3_pos(m1, up, B2);  // H + B (clamp at H = 0)
-                        gn[rw] = pk_add(hn, GAP2);
-                        // signs: D (up beats both), I (left beats the diagonal)
-                        ac[rw] = bfi(mk, sign_bytes(pk_sub(m1, up), pk_sub(dg, gl[rw])), ac[rw]);  // [I A, I B, D A, D B]
-                    }
-                    dv = gl[rw];
-                    up = gn[rw];
-                }
+                a0 = bfi(mk, sign_bytes(pk_sub(m10, up0), pk_sub(dg0, gl0)), a0);   // [I0A, I0B, D0A, D0B]
+                a1 = bfi(mk, sign_bytes(pk_sub(m11, gn0), pk_sub(dg1, gl1)), a1);   // [I1A, I1B, D1A, D1B]
                 if (kb >= 8 || kb + s >= lg) {  // (ramp: columns <= 0 keep the checkpoint)
-#pragma unroll
-                    for (int rw = 0; rw < kCkRows; ++rw) gl[rw] = gn[rw];
+                    gl0 = gn0;
+                    gl1 = gn1;
                 }
                 upp = up0;
             }
-#pragma unroll
-            for (int rw = 0; rw < kCkRows; ++rw) acc[rw][kb / 8] = ac[rw];
+            acc[0][kb / 8] = a0;
+            acc[1][kb / 8] = a1;
         };
         auto sweep = [&](auto tab_tag) {
             block(std::integral_constant<int, 0>{}, tab_tag);
@@ -492,15 +459,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             return w32 >> ((uint32_t)(32 - Wh) & 31u);
         };
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-#pragma unroll
-            for (int rw = 0; rw < kCkRows; ++rw) {
-                const uint32_t iw = word(acc[rw], (uint32_t)h, W[h]), dw = word(acc[rw], 2u + h, W[h]);
-                G.u.w.row[h][kCkRows * lg + rw] = make_uint2(~iw | dw, dw);
-            }
+        for (int h = 0; h < 2; ++h) {
+            const uint32_t i0 = word(acc[0], (uint32_t)h, W[h]), d0 = word(acc[0], 2u + h, W[h]);
+            const uint32_t i1 = word(acc[1], (uint32_t)h, W[h]), d1 = word(acc[1], 2u + h, W[h]);
+            G.row[h][2 * lg] = make_uint2(~i0 | d0, d0);
+            G.row[h][2 * lg + 1] = make_uint2(~i1 | d1, d1);
+        }
         ck_wave_sync();
 
-        // ---- the walk across the window, one row per step (lanes 0-1: pair A, 2-3: pair B):
+        // ---- the walk across the window, one row per step (lanes 0-3: pair A, 4-7: pair B):
         // the I run from the current column (up to the first NI bit, at most to column 0),
         // then the D or M move out of the row -- or, when the run reaches column c0, on in
         // the next window.  Flags as 0 / 1 integers; the loop keeps only what the next step
@@ -513,10 +480,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const bool room = nev + 2u * (uint32_t)(mr + 1) + 1u <= cap;
         uint32_t wl = (mlive && room) ? 1u : 0u, nrec = 0, pos = 0;
         int rr = mr;
-        const uint2* rp = &G.u.w.row[hh][rr - 1];  // the row a move up reaches (a walk only moves up)
-        uint16_t* recs = G.u.w.rec[hh];
-        uint16_t* recp = recs;                  // step k's record at recs[k] (the steps of a live walk are its records)
-        auto row_step = [&](const uint2& w2, uint16_t* rec) {
+        const uint2* rp = &G.row[hh][rr - 1];  // the row a move up reaches (a walk only moves up)
+        uint32_t* recs = G.rec[hh];
+        uint32_t* recp = recs;                  // step k's record at recs[k] (the steps of a live walk are its records)
+        auto row_step = [&](const uint2& w2, uint32_t* rec) {
             // (NI's bit W is set when W < 32; a run to the edge of a 32-column window finds no
             // NI bit, hence the 33rd bit and the bound)
             const uint32_t run = min((uint32_t)__builtin_ctzll((uint64_t)(w2.x >> pos) | (1ull << 32)), (uint32_t)mW - pos);
@@ -524,9 +491,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             const uint32_t edge = p1 >= (uint32_t)mW ? 1u : 0u;
             const uint32_t dmove = (w2.y >> (p1 & 31u)) & 1u;
             const uint32_t mv = wl & (edge ^ 1u);
-            *rec = (uint16_t)(run | (dmove << 8) | (edge << 9) | (p1 << 10));  // (p1: the move's column, bit W - x)
+            *rec = run | (dmove << 8) | (edge << 9) | (p1 << 10);  // (p1: the move's column, bit W - x)
             nrec += wl;
-            pos += (wl ? run : 0u) + (mv & (dmove ^ 1u));
+            pos += (wl ? run : 0u) + (mv & (dmove ^ 1u));  // (a select: v_mul_lo_u32 is quarter rate)
             rr -= (int)mv;
             wl = mv & ((uint32_t)~rr >> 31) & (pos < (uint32_t)mW ? 1u : 0u);
         };
@@ -551,68 +518,74 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         // carries its run to the next window.  Consecutive M moves with no I run between
         // them are one event, written at the run's last record (the formatter's work
         // goes with the events: ~1,000 a config-2 pair, about half of them M moves that
-        // continue an M run).  Records 8 lw .. 8 lw + 7 per lane; the pair's M-move and
-        // no-I-run masks over its 16 records are OR-ed over the pair's 2 lanes.
-        // (quad_perm: [1, 0, 3, 2] the pair's other lane; [0, 0, 2, 2] its first; [1, 1, 3, 3]
-        // its second -- each cross-lane move outside any select: inside `?:` one became a
-        // branch that masked its source lanes off, and a masked-off DPP source reads as the
-        // old value)
+        // continue an M run).  Records 4 lw .. 4 lw + 3 per lane; the pair's M-move and
+        // no-I-run masks over its 16 records are OR-ed over the pair's 4 lanes.
         bool zstop = false;
         if constexpr (LOCAL) {
             // the cost before record k: H(k + 1) = H(k) - gap (run + a D move) - s (an M move,
             // s of the cell it leaves: query row mr - k, column x = W - p1); the walk ends on
             // the first record k in 1 .. nrec with H(k) = 0 (a gap move never lowers H, so only
-            // after an M move).  Prefix over the pair's 2 lanes.
-            int dk[kCkRecs], sum = 0;
+            // after an M move).  Records 4 lw .. 4 lw + 3 per lane, prefix over the quad.
+            int dk[4], sum = 0;
 #pragma unroll
-            for (int h = 0; h < kCkRecs; ++h) {
-                const uint32_t k = (uint32_t)(kCkRecs * lw + h);
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h;
                 const uint32_t rc = k < nrec ? recs[k] : 0x200u;
                 const bool ed = rc & 0x200u, dm = rc & 0x100u;
                 const uint32_t x = (uint32_t)mW - ((rc >> 10) & 63u);  // (p1 <= W: x in 0 .. 32)
-                const uint32_t t = ((uint32_t)G.tbyte[x] >> (8 * hh)) & 0xFFu;
+                const uint2 tv = G.tb[8u + x];
                 const uint32_t q = G.qb[hh][(uint32_t)(mr - (int)k) & 15u];
-                const int sc = t == q ? ma : mi;
+                int sc;
+                if (tab) sc = (int)(((hh ? tv.y : tv.x) >> (8u * ((q >> 1) & 3u))) & 0xFFu) - 128 + gap;  // ck_gain_table
+                else sc = ((tv.x >> (16 * hh)) & 0xFFu) == q ? ma : mi;
                 dk[h] = -gap * (int)((rc & 63u) + (!ed && dm ? 1u : 0u)) - (!ed && !dm ? sc : 0);
                 sum += dk[h];
             }
-            const int s1 = (int)quad<0xA0>((uint32_t)sum);
-            const int inc = sum + (lw ? s1 : 0);
-            const int tot = (int)quad<0xF5>((uint32_t)inc);
-            int hk = mcost + inc - sum;  // H before record 8 lw
+            int inc = sum;
+            const int s1 = (int)quad<0x90>((uint32_t)inc);
+            inc += lw >= 1 ? s1 : 0;
+            const int s2 = (int)quad<0x40>((uint32_t)inc);
+            inc += lw >= 2 ? s2 : 0;
+            const int tot = (int)quad<0xFF>((uint32_t)inc);
+            int hk = mcost + inc - sum;  // H before record 4 lw
             uint32_t zf = 0;
 #pragma unroll
-            for (int h = 0; h < kCkRecs; ++h) {
-                const uint32_t k = (uint32_t)(kCkRecs * lw + h);
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h;
                 zf |= (k >= 1u && k <= nrec && hk == 0) ? 1u << k : 0u;
                 hk += dk[h];
             }
-            zf |= (lw == 1 && nrec >= 16u && hk == 0) ? 1u << 16 : 0u;  // after the 16th record
+            zf |= (lw == 3 && nrec >= 16u && hk == 0) ? 1u << 16 : 0u;  // after the 16th record
             const uint32_t z1 = quad<0xB1>(zf);
             zf |= z1;
+            const uint32_t z2 = quad<0x4E>(zf);
+            zf |= z2;
             const uint32_t kz = (uint32_t)__builtin_ctz(zf | (1u << 17));
             zstop = kz <= nrec;
             nrec = min(nrec, kz);
             mcost += tot;  // (stopped: no longer read)
         }
         {
-            uint32_t rcs[kCkRecs], mm = 0, zm = 0;
+            uint32_t rcs[4], mm = 0, zm = 0;
 #pragma unroll
-            for (int h = 0; h < kCkRecs; ++h) {
-                const uint32_t k = (uint32_t)(kCkRecs * lw + h);
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h;
                 rcs[h] = k < nrec ? recs[k] : 0x200u;  // (past the list: no event)
                 const uint32_t runI = (rcs[h] & 63u) + (k == 0 ? kI : 0u);
                 mm |= ((rcs[h] & 0x300u) == 0 ? 1u : 0u) << k;  // an M move
                 zm |= (runI == 0 ? 1u : 0u) << k;
             }
-            const uint32_t o1 = quad<0xB1>(mm), z1 = quad<0xB1>(zm);
+            const uint32_t o1 = quad<0xB1>(mm), z1 = quad<0xB1>(zm);  // quad_perm [1, 0, 3, 2]
             mm |= o1;
             zm |= z1;
+            const uint32_t o2 = quad<0x4E>(mm), z2 = quad<0x4E>(zm);  // quad_perm [2, 3, 0, 1]
+            mm |= o2;
+            zm |= z2;
             const uint32_t cont = mm & zm & (mm << 1);  // record k continues record k - 1's M run
-            uint32_t ev[2 * kCkRecs], ne = 0;
+            uint32_t ev[8], ne = 0;
 #pragma unroll
-            for (int h = 0; h < kCkRecs; ++h) {
-                const uint32_t k = (uint32_t)(kCkRecs * lw + h), rc = rcs[h];
+            for (int h = 0; h < 4; ++h) {
+                const uint32_t k = 4u * (uint32_t)lw + (uint32_t)h, rc = rcs[h];
                 const uint32_t runI = (rc & 63u) + (k == 0 ? kI : 0u);
                 const bool ed = rc & 0x200u, iev = !ed && runI > 0;
                 // an M run ending here: its first record is the last one at or below k that
@@ -625,14 +598,19 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                 ne |= (iev ? 1u : 0u) << (2 * h);
                 ne |= (!ed && ((rc & 0x100u) || mend) ? 1u : 0u) << (2 * h + 1);
             }
-            // exclusive prefix of the lane's event counts over the pair's 2 lanes
+            // exclusive prefix of the lane's event counts over the pair's 4 lanes
             const uint32_t cnt = (uint32_t)__builtin_popcount(ne);
-            const uint32_t s1 = quad<0xA0>(cnt);
-            const uint32_t inc = cnt + (lw ? s1 : 0u);
-            const uint32_t tot = quad<0xF5>(inc);
+            // (each cross-lane move outside the select: inside `?:` it became a branch that
+            // masked its source lanes off, and a masked-off DPP source reads as the old value)
+            uint32_t inc = cnt;
+            const uint32_t s1 = quad<0x90>(inc);  // quad_perm [0, 0, 1, 2]
+            inc += lw >= 1 ? s1 : 0u;
+            const uint32_t s2 = quad<0x40>(inc);  // quad_perm [0, 0, 0, 1]
+            inc += lw >= 2 ? s2 : 0u;
+            const uint32_t tot = quad<0xFF>(inc);  // quad_perm [3, 3, 3, 3]
             uint32_t at = nev + inc - cnt;
 #pragma unroll
-            for (int e = 0; e < 2 * kCkRecs; ++e) {
+            for (int e = 0; e < 8; ++e) {
                 if ((ne >> e) & 1u) rout[at] = ev[e];
                 at += (ne >> e) & 1u;
             }
@@ -667,8 +645,9 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             mdone = done;
             ml = !done && room && windows <= mnm + 16u;
         }
-        // (quad_perm [2, 3, 0, 1]: the other pair's walker)
-        const int oi = (int)quad<0x4E>((uint32_t)mi_), oj = (int)quad<0x4E>((uint32_t)mj), ol = (int)quad<0x4E>(ml ? 1u : 0u);
+        // (row_half_mirror: lane l <- lane 7 - l of its 8-lane group, the other pair's walker)
+        auto other = [](int v) { return __builtin_amdgcn_update_dpp(0, v, 0x141, 0xF, 0xF, false); };
+        const int oi = other(mi_), oj = other(mj), ol = other(ml ? 1 : 0);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
             const bool mine = h == hh;

@@ -151,28 +151,27 @@ def test_window_loads_in_bounds(n, m):
         c0 = np.where(e >= 16, np.maximum((e >> 4) * 16 - l, 0), 0)
         W = j - c0
         assert (W >= 1).all() and (W <= LEAD + 15).all()
-        for lg in range(4):  # a group's 4 lanes, rows 4 lg .. 4 lg + 3
-            li = np.where(c0 > 0, ck_col_index(g >> 6, (e >> 4) - 1, l, nb, 4 * lg), 0)
-            assert (li >= 0).all() and (li + 3 < region).all()
+        for lg in range(8):
+            li = np.where(c0 > 0, ck_col_index(g >> 6, (e >> 4) - 1, l, nb, 2 * lg), 0)
+            assert (li >= 0).all() and (li + 1 < region).all()
             if g > 0:
                 gu = g - 1
                 lu, pu = gu & 63, gu >> 6
                 t0 = c0 + lg + lu - 1
+                t1 = t0 + 8
                 base = pu * nb * 2048 + lu * 16
-                ib = [base + ((t0 + 4 * b) >> 4) * 1024 + ((t0 + 4 * b) & 15) for b in range(4)]
-                for q in range(9):  # columns x = lg + 4q, loaded only when x <= W
-                    x = lg + 4 * q
-                    ld = x <= W
-                    idx = np.maximum(ib[q & 3] + 1024 * (q >> 2), 0)[ld]
+                i0 = base + (t0 >> 4) * 1024 + (t0 & 15)
+                i1 = base + (t1 >> 4) * 1024 + (t1 & 15)
+                for q, idx in enumerate((np.maximum(i0, 0), i1, i0 + 1024, i1 + 1024, i0 + 2048)):
                     assert (idx >= 0).all() and (idx < region).all(), (n, m, i, lg, q)
-                    col = (c0 + x)[ld]
+                    col = c0 + lg + 8 * q
                     ok = col > 0
                     assert (idx[ok] == ck_row_index(pu, col[ok] + lu - 1, lu, nb)).all(), (n, m, i, lg, q)
-            for q in range(8):
-                x = 1 + lg + 4 * q
+            for q in range(4):
+                x = 1 + lg + 8 * q
                 tix = (c0 + x - 1)[x <= W]
                 assert (tix >= 0).all() and (tix < m).all()
-            assert 0 <= min(16 * g + 4 * lg + 3, n - 1) < n
+            assert 0 <= min(16 * g + 2 * lg + 1, n - 1) < n
 
 
 def kernel_events_walk(H, D, I, i, j, q, t, sc):
