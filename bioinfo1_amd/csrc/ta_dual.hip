@@ -76,6 +76,9 @@ struct DualIo {
     uint32_t* err;
     // blocked layout (BLK): this wave's LDS staging of 16 steps, [pair][step][lane]
     uint32_t* cbuf;
+    // CLS: this wave's per-step operands of the current 64 steps, entry k for step 64c + k:
+    // both pairs' tables of the target byte and the row above (dual_pass LST)
+    uint4* lst;
     uint32_t nb;  // blk_count(m)
 };
 
@@ -190,11 +193,21 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     uint32_t bestK = rep16(-16), bestj = 0;
     uint32_t rowbest = rep16(-32768), rowbest_j = 0;  // semi: best of row n, its column
 
+    // LST (CLS): a step's wave-uniform operands -- the two pairs' tables of the new target
+    // byte and the row above -- come from one LDS read of a 64-entry list each lane fills for
+    // its column every 64 steps, instead of three v_readlane and the SALU table arithmetic;
+    // the DPP hand-offs then take the read registers as their lane-0 value (no v_mov)
+    constexpr bool LST = CLS;
     uint32_t tcur[2], tnext[2];
+    auto tbyte = [&](int h, uint32_t c) -> uint32_t {  // target byte of step 64c + lane
+        const uint32_t k = c * 64u + (uint32_t)lane;
+        return k < m ? (uint32_t)io.T[h][k] : 0u;
+    };
+    auto table = [&](uint32_t b) -> uint32_t { return EQ ? class_table(b, T0, TX) : mismatch_table(b); };
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-        tcur[h] = load_tchunk(io.T[h], m, 0, lane);
-        tnext[h] = load_tchunk(io.T[h], m, 1, lane);
+        tcur[h] = LST ? tbyte(h, 0) : load_tchunk(io.T[h], m, 0, lane);
+        tnext[h] = LST ? tbyte(h, 1) : load_tchunk(io.T[h], m, 1, lane);
     }
     // The row above the pass, 64 columns per chunk (lane k: column 64c + k + 1):
     // the boundary row S(0, j) in pass 0, the previous pass's bottom row after.
@@ -206,6 +219,11 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
         return (int)rep16(LOCAL ? off + zstep * j - dl : (init - ma + gap) * j);
     };
     int bcur = top_chunk(0), bnext = top_chunk(1);
+    if constexpr (LST) {
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (after the last pass's reads)
+        io.lst[lane] = make_uint4(table(tcur[0]), table(tcur[1]), (uint32_t)bcur, 0u);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    }
     const uint32_t steps = m + nl - 1;
     uint32_t* prow0 = CIGAR ? io.ptrs[0] + (BLK ? (uint64_t)pass * io.nb * (kBlkSteps * kWave) : (uint64_t)pass * Tmax * kWave) : nullptr;
     uint32_t* prow1 = CIGAR ? io.ptrs[1] + (BLK ? (uint64_t)pass * io.nb * (kBlkSteps * kWave) : (uint64_t)pass * Tmax * kWave) : nullptr;
@@ -261,6 +279,16 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // Chunk reloads (every 256 steps: target bytes; every 64: the row above)
     // are hoisted out of the step loop by run_steps.
     auto reload = [&](uint32_t t) {
+        if constexpr (LST) {
+            // chunk t / 64's list (the reads of the last chunk's steps were issued before)
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+            io.lst[lane] = make_uint4(table(tnext[0]), table(tnext[1]), (uint32_t)bnext, 0u);
+            __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+            for (int h = 0; h < 2; ++h) tnext[h] = tbyte(h, (t >> 6) + 1);
+            bnext = top_chunk((t >> 6) + 1);
+            return;
+        }
         if ((t & 255u) == 0) {
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
@@ -273,23 +301,22 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     };
     auto step = [&](uint32_t t, auto masked_tag) {
         constexpr bool MASKED = decltype(masked_tag)::value;
-        const uint32_t top = (uint32_t)rdlane(bcur, t & 63u);
-        const uint32_t sh = (t & 3u) * 8;
-        const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
-        const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
-        const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
         const uint32_t prev = recv;
-        recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
-        if constexpr (UZ) recv = pk_add(recv, D2);
-        if constexpr (CLS && EQ) {
-            tA = (uint32_t)wave_shr1((int)class_table((wa >> sh) & 0xFFu, T0, TX), (int)tA);
-            tB = (uint32_t)wave_shr1((int)class_table((wb >> sh) & 0xFFu, T0, TX), (int)tB);
-        } else if constexpr (CLS) {
-            tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
-            tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
+        if constexpr (LST) {
+            const uint4 e = io.lst[t & 63u];  // (one address for the wave: a broadcast)
+            recv = (uint32_t)wave_shr1((int)e.z, (int)H2[R - 1]);
+            tA = (uint32_t)wave_shr1((int)e.x, (int)tA);
+            tB = (uint32_t)wave_shr1((int)e.y, (int)tB);
         } else {
+            const uint32_t top = (uint32_t)rdlane(bcur, t & 63u);
+            const uint32_t sh = (t & 3u) * 8;
+            const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
+            const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
+            const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
+            recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
             tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
         }
+        if constexpr (UZ) recv = pk_add(recv, D2);
         if constexpr (UZ) {
             zu += zstep;
         } else {
@@ -560,6 +587,7 @@ __device__ __forceinline__ void dual_fill_body(const FillArgs& a) {
     // (CK: the bottom row of each step, both pairs in one dword)
     constexpr int kStageDw = kDualCk ? 16 * kWave : 2 * kDualStage * kWave;
     __shared__ uint32_t cbuf_all[(BLK && kDualStage) ? kWavesPerBlock * kStageDw : 1];
+    __shared__ uint4 lst_all[kWavesPerBlock * 64];  // (dual_pass LST)
     uint32_t widx, p_only = 0;
     const bool pipe = a.ticket != nullptr;
     if (pipe) {
@@ -591,6 +619,7 @@ __device__ __forceinline__ void dual_fill_body(const FillArgs& a) {
     io.tag_w = io.tag_r = 0;
     io.err = a.err;
     io.cbuf = cbuf_all + ((BLK && kDualStage) ? (threadIdx.x >> 6) * kStageDw : 0);
+    io.lst = lst_all + (threadIdx.x >> 6) * 64;
     io.nb = blk_count(m);
     bool dash = false, qother = false;
 #pragma unroll

@@ -8,8 +8,9 @@
    use (8 independent chains x 8 waves per SIMD: throughput, not latency).
    The measured values sit ~5-30 % above the issue class (loop overhead);
    each opcode is assigned its class, 2 or 4 cycles (the nearest of 2, 4, 8, 16).
-2. Instruction mix: a static census of the kernel's hot loop (the loop with the
-   most DPP hand-offs) in the gfx950 assembly of its translation unit.
+2. Instruction mix: a static census of the kernel's step loop (the innermost
+   loop with the most DPP hand-offs, scripts/isa_census.py) in the gfx950
+   assembly of its translation unit.
 3. Mixed roof: cycles per wave-instruction = census-weighted mean of the
    classes; peak = 256 CU x 4 SIMD x 64 lanes x 2.4 GHz / that mean, in VALU
    lane-operations per second -- the number bench.py's valu.frac divides by.
@@ -95,26 +96,13 @@ def asm_of(src, defines):
 
 
 def census(src, defines, sym):
-    text = asm_of(src, defines)
-    funcs = re.split(r"\n(?=_Z\w+:)", text)
-    body = [f for f in funcs if f.split(":")[0].find(sym) >= 0 and "s_endpgm" in f][0].split(".Lfunc_end")[0]
-    lines = body.splitlines()
-    labels = {m.group(1): k for k, ln in enumerate(lines) if (m := re.match(r"^(\.LBB\w+):", ln))}
-    best = None
-    for k, ln in enumerate(lines):
-        m = re.search(r"s_cbranch_\w+\s+(\.LBB\w+)|s_branch\s+(\.LBB\w+)", ln)
-        if m:
-            t = m.group(1) or m.group(2)
-            if t in labels and labels[t] < k:
-                c = collections.Counter()
-                for x in lines[labels[t]:k + 1]:
-                    tok = x.strip().split()
-                    if tok and tok[0].startswith("v_"):
-                        c[tok[0]] += 1
-                dpp = sum(v for o, v in c.items() if "_dpp" in o)
-                if best is None or dpp > best[0]:
-                    best = (dpp, c)
-    return best[1]
+    """VALU opcodes of the kernel's step loop (scripts/isa_census.py step_loop: the innermost
+    loop with the most DPP moves, then the most three-input maxima, then the fewest VALU)."""
+    import isa_census
+
+    lines = isa_census.function_lines(asm_of(src, defines), sym)
+    _, c = isa_census.step_loop(lines)
+    return collections.Counter({o: n for o, n in c.items() if o.startswith("v_")})
 
 
 def roof(mix, rates):
