@@ -618,6 +618,8 @@ def dominant_kernel(plan, mode, cigar, affine):
     if affine:
         return f"affine_dual_fill_kernel<{mode}, {c}>" if plan.dual_pairs else f"affine_fill_kernel<{mode}, {c}>"
     if plan.flex_pairs and plan.flex_pairs * 2 >= plan.P:
+        if cigar and getattr(plan, "ck", False):
+            return f"flex_fill_ck_kernel<{mode}>"  # (checkpoints instead of codes)
         return f"flex_fill_kernel<{mode}, {c}>"
     if plan.dual_pairs * 2 >= plan.P:
         if cigar and getattr(plan, "ck", False):
@@ -628,7 +630,7 @@ def dominant_kernel(plan, mode, cigar, affine):
 
 # The translation unit each kernel is compiled from (build.sh), by rocprof-name prefix.
 KERNEL_TU = (("dual_fill_ck_kernel", "ta_dual.hip"), ("dual_fill_kernel", "ta_dual.hip"),
-             ("flex_fill_kernel", "ta_flex.hip"), ("affine_", "ta_affine.hip"),
+             ("flex_fill_ck_kernel", "ta_flex.hip"), ("flex_fill_kernel", "ta_flex.hip"), ("affine_", "ta_affine.hip"),
              ("traceback_ck_kernel", "ta_walk_ck.hip"), ("fill_kernel", "ta_kernels.hip"),
              ("traceback", "ta_kernels.hip"), ("format_runs_kernel", "ta_kernels.hip"))
 CSRC = os.path.join(ROOT, "bioinfo1_amd", "csrc")

@@ -30,6 +30,7 @@ TA_OK, TA_ERR_BAD_TYPE, TA_ERR_CIGAR, TA_ERR_ARG, TA_ERR_DEVICE, TA_ERR_CAPACITY
 # ta_plan_create flags (include/team_align_c.h): kernel selection, same results
 TA_PLAN_INT32_ONLY, TA_PLAN_NO_FLEX, TA_PLAN_UNFUSED, TA_PLAN_WALK1, TA_PLAN_WALK2 = 1, 2, 4, 8, 16
 TA_PLAN_SERIAL_PASSES, TA_PLAN_PASS_MAJOR, TA_PLAN_NO_BLK, TA_PLAN_NO_CK, TA_PLAN_CK = 32, 64, 128, 256, 512
+TA_PLAN_NO_FLEX_CK = 1024
 
 
 class AlignmentType(enum.IntEnum):

@@ -197,7 +197,9 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
     // byte and the row above -- come from one LDS read of a 64-entry list each lane fills for
     // its column every 64 steps, instead of three v_readlane and the SALU table arithmetic;
     // the DPP hand-offs then take the read registers as their lane-0 value (no v_mov)
-    constexpr bool LST = CLS;
+    // (not in the code fill of blocked plans: its 32 KB of staging per block leave no room
+    // for the list at 5 waves per SIMD)
+    constexpr bool LST = CLS && (!BLK || kDualCk);
     uint32_t tcur[2], tnext[2];
     auto tbyte = [&](int h, uint32_t c) -> uint32_t {  // target byte of step 64c + lane
         const uint32_t k = c * 64u + (uint32_t)lane;
@@ -314,7 +316,12 @@ __device__ __forceinline__ DualOut dual_pass(const FillArgs& a, const DualIo& io
             const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
             const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
             recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
-            tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+            if constexpr (CLS) {
+                tA = (uint32_t)wave_shr1((int)table((wa >> sh) & 0xFFu), (int)tA);
+                tB = (uint32_t)wave_shr1((int)table((wb >> sh) & 0xFFu), (int)tB);
+            } else {
+                tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+            }
         }
         if constexpr (UZ) recv = pk_add(recv, D2);
         if constexpr (UZ) {
@@ -587,7 +594,7 @@ __device__ __forceinline__ void dual_fill_body(const FillArgs& a) {
     // (CK: the bottom row of each step, both pairs in one dword)
     constexpr int kStageDw = kDualCk ? 16 * kWave : 2 * kDualStage * kWave;
     __shared__ uint32_t cbuf_all[(BLK && kDualStage) ? kWavesPerBlock * kStageDw : 1];
-    __shared__ uint4 lst_all[kWavesPerBlock * 64];  // (dual_pass LST)
+    __shared__ uint4 lst_all[(BLK && !kDualCk) ? 1 : kWavesPerBlock * 64];  // (dual_pass LST)
     uint32_t widx, p_only = 0;
     const bool pipe = a.ticket != nullptr;
     if (pipe) {

@@ -52,6 +52,15 @@ namespace {
 #ifndef TA_SWAR
 #define TA_SWAR 1
 #endif
+// CK (with TA_FLEX_CIGAR, a translation unit of its own): checkpoints instead of codes,
+// in the dual fill's layout (ta_layout.h ck_row_index / ck_col_index, each pair with its
+// own block count) and as H itself -- the frame of V (rebased every 64 steps, a lane
+// frame in local mode) taken out at the store -- for the recomputing walk
+// (ta_walk_ck.hip), which tells these pairs by their flag (2)
+#ifndef TA_FLEX_CK
+#define TA_FLEX_CK 0
+#endif
+constexpr bool kFlexCk = TA_FLEX_CK != 0;
 
 __device__ __forceinline__ int sext_lo(uint32_t x) { return (int)(int16_t)(x & 0xFFFFu); }
 __device__ __forceinline__ int sext_hi(uint32_t x) { return (int)(int16_t)(x >> 16); }
@@ -77,6 +86,7 @@ struct FlexIo {
     const uint64_t* rec_r;  // the previous pass's (null on pass 0)
     uint32_t tag_w, tag_r;
     uint32_t* err;
+    uint32_t* cbuf;  // CK: this wave's LDS staging of 16 steps' bottom rows, [step][lane]
 };
 
 struct FlexOut {
@@ -128,6 +138,8 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     const uint32_t nl = (nrows + R - 1) / R;
     const uint32_t nlh[2] = {nl, (min((uint32_t)kPassRows, io.n[1] - row_base) + R - 1) / R};
     const bool has_next = !last_pass;
+    constexpr bool CK = kFlexCk && CIGAR;
+    constexpr bool CODES = CIGAR && !CK;
 
     constexpr bool LOCAL = MODE == kLocal;
     // local: every value is kept in [0, 0x7BFF] (flex_local_fits) so the clamp
@@ -179,8 +191,58 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     if (pass > 0) load_rec_chunk(io, M, 0, lane, bcur);
     const uint32_t steps = M + nl - 1;
     const uint32_t Tmax0 = pass_steps(io.m[0]), Tmax1 = pass_steps(io.m[1]);
-    uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * Tmax0 * kWave : nullptr;
-    uint32_t* prow1 = CIGAR ? io.ptrs[1] + (uint64_t)pass * Tmax1 * kWave : nullptr;
+    // CK: each pair's blocks of this pass (ta_layout.h ck_row_index: nb_h * 1024 dwords a pass)
+    const uint32_t nbh[2] = {blk_count(io.m[0]), blk_count(io.m[1])};
+    uint32_t* prow0 = CIGAR ? io.ptrs[0] + (uint64_t)pass * (CK ? nbh[0] * (kBlkSteps * kWave) : Tmax0 * kWave) : nullptr;
+    uint32_t* prow1 = CIGAR ? io.ptrs[1] + (uint64_t)pass * (CK ? nbh[1] * (kBlkSteps * kWave) : Tmax1 * kWave) : nullptr;
+    // CK, global / semi: H = V + O + (ma - gap) j + gap i for the cell of row i, column j,
+    // j = t - l + 1 at step t: the lane's part for its bottom row (i = 16 (l + 1) in the
+    // pass); the step's part, O + (ma - gap) (t + 1), is per pair and wave-uniform (ck_step)
+    const uint32_t KLB = rep16(-(ma - rowb) * lane + rowb * (int)(row_base + (uint32_t)(lane + 1) * R));
+    auto ck_step = [&](uint32_t t, int c) -> uint32_t {  // (+ c in each half)
+        const int u = (ma - rowb) * (int)(t + 1) + c;
+        return ((uint32_t)(O[0] + u) & 0xFFFFu) | ((uint32_t)(O[1] + u) << 16);
+    };
+    // CK: H of row r from its value (local: above the row's clamp base zu - gap r, the
+    // lane frame and O cancel, ta_flex.hip header)
+    auto ck_h = [&](uint32_t v, int r, uint32_t t) -> uint32_t {
+        if constexpr (LOCAL) return pk_sub(v, rep16(zu - gap * r));
+        else return pk_add(pk_add(v, KLB), ck_step(t, -rowb * (R - 1 - r)));
+    };
+    // every 16 steps (and at the pass's end): the staged bottom rows of the steps up to t,
+    // and at a block's end (full) the 16 rows, both split by pair (v_perm); pair B only
+    // within its own blocks
+    auto ck_flush = [&](uint32_t t, bool full) {
+        const uint32_t b = t >> 4;
+        uint32_t x[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) x[q] = io.cbuf[q * kWave + lane];
+        uint32_t hr[R];
+        if (full) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) hr[r] = ck_h(H2[r], r, t);
+        }
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            if (b >= nbh[h]) continue;
+            const uint32_t sel = h ? 0x07060302u : 0x05040100u;
+            uint32_t* dr = (h ? prow1 : prow0) + ((uint64_t)b * kWave + (uint32_t)lane) * 8u;
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int q = 0; q < 2; ++q)
+                *reinterpret_cast<uint4*>(dr + 4 * q) =
+                    make_uint4(__builtin_amdgcn_perm(x[8 * q + 1], x[8 * q], sel), __builtin_amdgcn_perm(x[8 * q + 3], x[8 * q + 2], sel),
+                               __builtin_amdgcn_perm(x[8 * q + 5], x[8 * q + 4], sel), __builtin_amdgcn_perm(x[8 * q + 7], x[8 * q + 6], sel));
+            if (full) {
+                uint32_t* dc = dr + (uint64_t)nbh[h] * kWave * 8u;
+#pragma unroll
+                for (int q = 0; q < 2; ++q)
+                    *reinterpret_cast<uint4*>(dc + 4 * q) =
+                        make_uint4(__builtin_amdgcn_perm(hr[8 * q + 1], hr[8 * q], sel), __builtin_amdgcn_perm(hr[8 * q + 3], hr[8 * q + 2], sel),
+                                   __builtin_amdgcn_perm(hr[8 * q + 5], hr[8 * q + 4], sel), __builtin_amdgcn_perm(hr[8 * q + 7], hr[8 * q + 6], sel));
+            }
+        }
+    };
 
     auto reload = [&](uint32_t t) {
         if ((t & 255u) == 0) {
@@ -287,7 +349,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 uint32_t hv;
                 if constexpr (LOCAL) hv = pk_max3_pos_bc<r & 1>(m1, up, W[r / 2]);  // clamp folded in, :185
                 else hv = pk_max(m1, up);
-                if (CIGAR) {
+                if (CODES) {
                     // raw compares (D wins over I in the walk; local walks track the cost)
                     const uint32_t wd = pk_sub_sat(m1, up);
                     const uint32_t wi = pk_sub_sat(diag, left);
@@ -349,7 +411,9 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         // column m_h reached by some lane this step (uniform window test)
         if (!LOCAL && t + 1 >= io.m[0] && t + 1 < io.m[0] + kWave) capture(0, j, active);
         if (!LOCAL && t + 1 >= io.m[1] && t + 1 < io.m[1] + kWave) capture(1, j, active);
-        if (CIGAR) {
+        if constexpr (CK) {
+            io.cbuf[(t & 15u) * kWave + (uint32_t)lane] = ck_h(H2[R - 1], R - 1, t);  // (flushed by run_steps)
+        } else if (CIGAR) {
             const uint32_t off = (t * kWave + (uint32_t)lane) * 4u;
             if (t < Tmax0) *(uint32_t*)((char*)prow0 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x06020400u);
             if (t < Tmax1) *(uint32_t*)((char*)prow1 + off) = __builtin_amdgcn_perm(acc0, acc1, 0x07030501u);
@@ -363,12 +427,16 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
                 reload(t);
                 next_reload += 64;
             }
-            const uint32_t blk = min(t_end, next_reload);
+            uint32_t blk = min(t_end, next_reload);
+            if constexpr (CK) blk = min(blk, (t | 15u) + 1u);  // (the flushes outside the step body)
             for (; t + 1 < blk; t += 2) {  // steps in pairs (as ta_dual.hip)
                 step(t, masked_tag);
                 step(t + 1, masked_tag);
             }
             if (t < blk) step(t++, masked_tag);
+            if constexpr (CK) {
+                if ((t & 15u) == 0 || t == steps) ck_flush(t - 1, (t & 15u) == 0);
+            }
         }
     };
     run_steps(ramp_end, std::true_type{});
@@ -441,8 +509,10 @@ constexpr uint32_t kSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to the 
 // long after its predecessor, instead of all passes of a couple starting
 // together and each waiting for the one above.
 template <int MODE, bool CIGAR>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_WAVES))) void flex_fill_kernel(FillArgs a) {
+__device__ __forceinline__ void flex_fill_body(FillArgs a) {
     const int lane = threadIdx.x & 63;
+    constexpr bool CK = kFlexCk && CIGAR;
+    __shared__ uint32_t cbuf_all[CK ? kWavesPerBlock * 16 * kWave : 1];
     uint32_t tk = 0;
     if (lane == 0) tk = atomicAdd(a.ticket, 1u);
     tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
@@ -470,7 +540,15 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
         }
     }
     PassOut* po = static_cast<PassOut*>(a.pout) + 2ull * g;
-    if (__ballot(qdash)) {  // per-row up gains: the int32 fill takes the couple (pass 0's wave hands it over)
+    // per-row up gains ('-' in a query) -- and with checkpoints any '-', whose free gap
+    // steps the recomputing walk does not model: the int32 fill takes the couple (pass
+    // 0's wave hands it over); CK: the walk's flag, 1 handed back, 2 a pair of this fill
+    const bool back = __ballot(qdash) || (CK && __ballot(tdash));
+    if (CK && a.pflag && lane == 0 && pass == 0) {
+        a.pflag[p[0]] = back ? 1 : 2;
+        a.pflag[p[1]] = back ? 1 : 2;
+    }
+    if (back) {
         if (lane == 0) {
             if (pass == 0) {
                 const uint32_t k = (p[1] != p[0]) ? 2u : 1u;
@@ -496,6 +574,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
     io.tag_w = a.epoch * 64u + pass + 1u;
     io.tag_r = a.epoch * 64u + pass;
     io.err = a.err;
+    io.cbuf = cbuf_all + (CK ? (threadIdx.x >> 6) * 16 * kWave : 0);
     const FlexOut o = __ballot(qother) == 0 ? flex_pass_nv<MODE, CIGAR, true>(a, io, pass, last_pass, tdash, lane)
                                             : flex_pass_nv<MODE, CIGAR, false>(a, io, pass, last_pass, tdash, lane);
     if (lane == 0) {
@@ -503,6 +582,18 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_
         po[1] = o.o[1];
     }
 }
+
+template <int MODE, bool CIGAR>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_WAVES))) void flex_fill_kernel(FillArgs a) {
+    flex_fill_body<MODE, CIGAR>(a);
+}
+#if TA_FLEX_CK
+// the checkpoint fill under a name of its own (rocprof, profiles/*_by_kernel.json)
+template <int MODE>
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(TA_FLEX_WAVES))) void flex_fill_ck_kernel(FillArgs a) {
+    flex_fill_body<MODE, true>(a);
+}
+#endif
 
 // After the fill: fold each couple's per-pass results in pass order (the
 // upper pass wins ties; semi: row n after column m, :265-278).
@@ -545,12 +636,27 @@ __global__ void flex_combine_kernel(FillArgs a) {
 }  // namespace
 
 #ifdef TA_FLEX_MODE
+#if TA_FLEX_CK
+template <>
+hipError_t launch_flex_ck<TA_FLEX_MODE>(const FillArgs& a, hipStream_t s) {
+    static_assert(TA_FLEX_CIGAR, "checkpoints replace the codes");
+#else
 template <>
 hipError_t launch_flex_mode<TA_FLEX_MODE, (TA_FLEX_CIGAR != 0)>(const FillArgs& a, hipStream_t s) {
+#endif
     if (!a.count) return hipSuccess;
+#if TA_FLEX_CIGAR && !TA_FLEX_CK
+    if (a.blk == 2) return launch_flex_ck<TA_FLEX_MODE>(a, s);  // (checkpoint plans)
+#endif
+#if TA_FLEX_CK
+    if (a.n_tasks)
+        hipLaunchKernelGGL(flex_fill_ck_kernel<TA_FLEX_MODE>, dim3((a.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock),
+                           dim3(kBlock), 0, s, a);
+#else
     if (a.n_tasks)
         hipLaunchKernelGGL((flex_fill_kernel<TA_FLEX_MODE, TA_FLEX_CIGAR != 0>),
                            dim3((a.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock), dim3(kBlock), 0, s, a);
+#endif
     hipLaunchKernelGGL((flex_combine_kernel<TA_FLEX_MODE>), dim3((a.count + 255) / 256), dim3(256), 0, s, a);
     return hipGetLastError();
 }

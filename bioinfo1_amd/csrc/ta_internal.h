@@ -182,6 +182,9 @@ hipError_t launch_dual_ck(const FillArgs& a, hipStream_t s);
 // The recomputing walks of checkpoint plans (ta_walk_ck.hip; TraceArgs.blk == 2), then
 // the fallback walk of the handed-back pairs; format_runs_kernel follows.
 hipError_t launch_walk_ck(int mode, const TraceArgs& a, hipStream_t s);
+// the flexible fill with checkpoints (ta_flex.hip TA_FLEX_CK), any mode
+template <int MODE>
+hipError_t launch_flex_ck(const FillArgs& a, hipStream_t s);
 // Flexible two-pair fill (ta_flex.hip, global / semi-global): a.order holds 2
 // pair ids per wave, the larger n first; both with the same pass count and
 // n mod 16; rebased int16 values, so any length fits.

@@ -39,6 +39,20 @@ bool flex_local_fits(uint32_t n, uint32_t m, int ma, int mi, int gap) {
     return mag <= 64 && hi <= 0x7BFF && hmax + 3LL * kWave * std::llabs(ma) + 8 * mag <= 30000;
 }
 
+// Checkpoints of the flexible fill hold H itself as int16 (ta_flex.hip CK), and the
+// recomputing walk keeps a window of a global / semi pair as S minus its corner's bias
+// part, H plus at most (|gap| + |gap - ma|) x 48 (ta_walk_ck.hip): H must lie within
+// +-30,000 for rows to n + 15 (semi H >= gap min(i, j), global (i + j) min(0, gap);
+// H <= hs min(i, j) + (i + j) max(0, gap)); local values also meet flex_local_fits.
+bool flex_ck_fits(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {
+    const long long N = (long long)n + 16, M = m, g = gap, K = std::min(N, M);
+    const long long mag = std::max({1LL, std::llabs(ma), std::llabs(mi), std::llabs(gap)});
+    const long long hi = K * std::max({0LL, (long long)ma, (long long)mi}) + (N + M) * std::max(0LL, g);
+    const long long lo = mode == kLocal ? 0 : mode == kSemi ? K * std::min(0LL, g) : (N + M) * std::min(0LL, g);
+    return lo - 100 * mag >= -30000 && hi + 100 * mag <= 30000 &&
+           (mode != kLocal || flex_local_fits(n, m, ma, mi, gap));
+}
+
 // Bounds of the biased 16-bit values of ta_dual.hip (S and every candidate),
 // with a margin; pairs that do not fit run in the int32 kernel.
 bool fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int gap) {
@@ -233,6 +247,20 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     };
     std::vector<Unit> units;
     units.reserve(n_pairs);
+    // Checkpoints save the fill ~0.3 of its time but the recomputing walk is a
+    // longer chain per pair than the band walk (one window per 16 rows): they pay
+    // once the cells per unit of the longest path pass ~2.5e6 (1 kb pairs: from
+    // ~5,000 pairs on; 8 to 4,096 measured slower, profiles/bench/r05_ck_batches.txt).
+    uint64_t cells = 0, longest = 1;
+    for (uint32_t p = 0; p < n_pairs; ++p) {
+        cells += (uint64_t)qlen[p] * tlen[p];
+        longest = std::max<uint64_t>(longest, (uint64_t)qlen[p] + tlen[p]);
+    }
+    const bool ck_size = (flags & kPlanCk) || cells >= 2500000ull * longest;
+    // a plan that may take checkpoints couples its leftover ragged pairs with themselves in
+    // the flexible fill (not the int32 fill, which only stores codes)
+    const bool ck_want = want_cigar && ck_size && mag < (1ull << 22) && (type != kLocal || gap <= 0) &&
+                         !(flags & (kPlanNoCk | kPlanNoBlk | kPlanWalk1 | kPlanWalk2));
     std::vector<uint32_t> rest;
     const bool flex_ok = dual && !(flags & kPlanNoFlex) && flex_fits(type, match, mismatch, gap);
     // A pair left without a partner (an odd pair of equal shapes, a ragged pair no
@@ -277,7 +305,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
         // lane), neighbours by (n, m), at most 25 % of the wave's cells wasted
         std::vector<uint32_t> cand;
         for (uint32_t p : rest) {
-            if (qlen[p] && tlen[p] && (type != kLocal || flex_local_fits(qlen[p], tlen[p], match, mismatch, gap)))
+            if (qlen[p] && tlen[p] && (type != kLocal || flex_local_fits(qlen[p], tlen[p], match, mismatch, gap)) &&
+                (!ck_want || flex_ck_fits(type, qlen[p], tlen[p], match, mismatch, gap)))
                 cand.push_back(p);
             else
                 units.push_back({0, p, p, (uint64_t)qlen[p] * tlen[p]});
@@ -304,7 +333,7 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
             // a long pair without a partner is coupled with itself: one wave per pass;
             // a shorter one in the dual kernel when it fits int16 (lone_dual)
             const uint32_t ps = n_passes(qlen[A]);
-            if (ps >= 4 && ps < 64)
+            if ((ps >= 4 || (ck_want && !lone_dual(A))) && ps < 64)
                 units.push_back({2, A, A, (uint64_t)qlen[A] * tlen[A]});
             else
                 units.push_back({lone_dual(A) ? 1 : 0, A, A, (uint64_t)qlen[A] * tlen[A]});
@@ -324,25 +353,28 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     // (batches of fewer than 8 pairs -- drop-in calls -- keep the lane walks: one band-walk
     // lane per pair leaves a lone wave's dependent chain ~50 us longer for 1-2 pairs of
     // 1 kb, scripts/exp/batch_latency.py, profiles/bench/r05_batch_latency.txt)
-    bool all_dual = !units.empty();
-    for (const Unit& u : units) all_dual = all_dual && u.kind == 1;
-    // Checkpoints save the fill ~0.3 of its time but the recomputing walk is a
-    // longer chain per pair than the band walk (one window per 16 rows): they pay
-    // once the cells per unit of the longest path pass ~2.5e6 (1 kb pairs: from
-    // ~5,000 pairs on; 8 to 4,096 measured slower, profiles/bench/r05_ck_batches.txt).
-    uint64_t cells = 0, longest = 1;
-    for (uint32_t p = 0; p < n_pairs; ++p) {
-        cells += (uint64_t)qlen[p] * tlen[p];
-        longest = std::max<uint64_t>(longest, (uint64_t)qlen[p] + tlen[p]);
+    bool all_dual = !units.empty(), all_packed = !units.empty(), any_flex = false;
+    for (const Unit& u : units) {
+        all_dual = all_dual && u.kind == 1;
+        all_packed = all_packed && u.kind >= 1;
+        any_flex = any_flex || u.kind == 2;
     }
-    const bool ck_size = (flags & kPlanCk) || cells >= 2500000ull * longest;
     // Global / semi-global plans of equal-shape couples (config 5) take checkpoints
     // and recomputing walks by the same rule, whatever their lengths: their walks end
     // on row 0 / column 0 (ta_walk_ck.hip) and need no cost, so no gap-sign condition.
     const bool edge_ck = want_cigar && type != kLocal && all_dual && mag < (1ull << 22) && ck_size &&
                          !(flags & (kPlanNoCk | kPlanNoBlk | kPlanWalk1 | kPlanWalk2));
+    // Plans with flexible couples (config 3: ragged reads) in any mode, when every unit
+    // is packed and every flexible pair's H fits the checkpoints (flex_ck_fits; local
+    // walks need gap <= 0, ck_want)
+    bool flex_fit = true;
+    for (const Unit& u : units)
+        if (u.kind == 2)
+            flex_fit = flex_fit && flex_ck_fits(type, qlen[u.a], tlen[u.a], match, mismatch, gap) &&
+                       flex_ck_fits(type, qlen[u.b], tlen[u.b], match, mismatch, gap);
+    const bool flex_ck = ck_want && any_flex && all_packed && flex_fit && !(flags & kPlanNoFlexCk);
     pl.blk = (want_cigar && type == kLocal && all_dual && short_pairs && n_pairs >= 8 && mag < (1ull << 22) &&
-              !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2))) || edge_ck;
+              !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2))) || edge_ck || flex_ck;
     // Multi-pass int32 pairs run one wave per (pair, pass) like the packed
     // fills (their passes overlap instead of following each other on one
     // wave); the walk then runs in the traceback kernel.

@@ -25,6 +25,7 @@ constexpr uint32_t kPlanPassMajor = 64u;     // pass tasks ticketed start-aligne
 constexpr uint32_t kPlanNoBlk = 128u;        // keep the [step][lane] code layout (no band walks)
 constexpr uint32_t kPlanNoCk = 256u;         // blk plans: codes + band walks, not checkpoints + recomputing walks
 constexpr uint32_t kPlanCk = 512u;           // blk plans: checkpoints + recomputing walks at any batch size
+constexpr uint32_t kPlanNoFlexCk = 1024u;    // plans with flexible couples: codes, not checkpoints
 
 // Can an n x m pair run in the packed int16 kernel (ta_dual.hip) without overflow?
 bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
@@ -32,6 +33,8 @@ bool fits_int16(int mode, uint32_t n, uint32_t m, int match, int mismatch, int g
 bool flex_fits(int mode, int match, int mismatch, int gap);
 // ... and, local mode, a pair whose scores stay within its int16 range.
 bool flex_local_fits(uint32_t n, uint32_t m, int match, int mismatch, int gap);
+// Do a flexible pair's H values fit the flexible fill's checkpoints (int16, with the walk's margin)?
+bool flex_ck_fits(int mode, uint32_t n, uint32_t m, int match, int mismatch, int gap);
 // Every packed value of the affine dual fill (ta_affine.hip) within int16.
 bool affine_fits_int16(int mode, uint32_t n, uint32_t m, int ma, int mi, int open, int ext);
 

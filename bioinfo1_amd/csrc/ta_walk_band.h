@@ -207,7 +207,7 @@ __device__ __forceinline__ void traceback_band_local(const TraceArgs& a, uint8_t
     const uint32_t k = 64u * blockIdx.x + (uint32_t)lane;
     bool has = k < a.count;
     const uint32_t p = has ? (a.order ? a.order[a.begin + k] : a.begin + k) : 0u;
-    if (has && a.pflag && a.pflag[p]) has = false;  // '-' bytes: the fallback walk (traceback_kernel)
+    if (has && a.pflag && a.pflag[p] == 1) has = false;  // '-' bytes: the fallback walk (traceback_kernel)
     uint32_t n = 0, m = 0, gi = 0, gj = 0;
     int H = 0;
     const uint32_t* P = a.ptrs;
@@ -450,7 +450,7 @@ __device__ __forceinline__ void bw_put_run(char* q, uint32_t c, uint32_t op, uin
 // events per round (RunWriter's layout, ta_device.h; "1\0" for no move,
 // :145-160).  A run still open at the end of a round is carried into the next.
 __device__ __forceinline__ void format_runs(const TraceArgs& a, uint32_t p, int lane) {
-    if (a.pflag && a.pflag[p]) return;  // walked by the fallback walk
+    if (a.pflag && a.pflag[p] == 1) return;  // walked by the fallback walk (2: a flexible-fill pair, walked over checkpoints)
     const uint32_t n = a.qlen[p], m = a.tlen[p];
     const uint64_t cap = cigar_slot_bytes(n, m), soff = a.slot_off[p];
     const uint32_t* ev = a.runs + band_runs_off(soff);

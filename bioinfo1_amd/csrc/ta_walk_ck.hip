@@ -122,6 +122,7 @@ __device__ __forceinline__ uint32_t quad(uint32_t v) {
 struct CkPair {
     uint32_t p, n, m, nb;
     int off, z, dl;  // the fill's frame (ta_layout.h ck_decode)
+    bool fx;         // a pair of the flexible fill (pflag 2): its checkpoints hold H itself
     const uint16_t* P;
     const uint8_t* Q;
     const uint8_t* T;
@@ -158,7 +159,10 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
         const uint32_t slot = ((blockIdx.x * kWavesPerBlock + (threadIdx.x >> 6)) * kCkGroups + (uint32_t)(lane >> 3)) * 2 + h;
         c.has = slot < a.count;
         c.p = c.has ? (a.order ? a.order[a.begin + slot] : a.begin + slot) : 0u;
-        if (c.has && a.pflag && a.pflag[c.p]) c.has = false;  // '-' bytes: the fallback walk
+        // the fills' flag: 1 handed back ('-' bytes: the fallback walk), 2 the flexible fill's
+        const uint32_t pf = (c.has && a.pflag) ? a.pflag[c.p] : 0u;
+        if (pf == 1u) c.has = false;
+        c.fx = pf == 2u;
         c.n = c.m = 0;
         c.P = reinterpret_cast<const uint16_t*>(a.ptrs);
         c.Q = a.qbytes;
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             c.T += a.toff[c.p];
         }
         // the checkpoint fill's frame (ck_decode): the equal-gain one with three-input maxima
-        const int off3 = (LOCAL && c.has) ? local_max3_offset(c.n, c.m, ma, mi, gap, true) : -1;
+        const int off3 = (LOCAL && c.has && !c.fx) ? local_max3_offset(c.n, c.m, ma, mi, gap, true) : -1;
         c.off = off3 >= 0 ? off3 : 0;
         c.z = local_max3_z(ma, off3 >= 0);
         c.dl = off3 >= 0 ? c.z + 16 : 0;
@@ -309,8 +313,11 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
             // column 0 (c0 = 0, x = 0): the boundary
             const uint32_t m0 = mT & (lg == 0 ? ((c0[0] > 0 ? 0xFFFFu : 0u) | (c0[1] > 0 ? 0xFFFF0000u : 0u)) : ~0u);
             if constexpr (LOCAL) {
-                gl0 = vsel(mL0, pk_lshr4(pk_add(l0, cl)), GB2);
-                gl1 = vsel(mL1, pk_lshr4(pk_add(l1, pk_add(cl, ONE))), GB2);
+                // (flexible-fill pairs: H itself, + gap + B)
+                const uint32_t fx = (S[0].fx ? 0xFFFFu : 0u) | (S[1].fx ? 0xFFFF0000u : 0u);
+                auto dec = [&](uint32_t v, uint32_t c) { return vsel(fx, pk_add(v, GB2), pk_lshr4(pk_add(v, c))); };
+                gl0 = vsel(mL0, dec(l0, cl), GB2);
+                gl1 = vsel(mL1, dec(l1, pk_add(cl, ONE)), GB2);
                 // the decode constant moves by -z per column
                 const uint32_t dx = ((uint32_t)(-8 * S[0].z) & 0xFFFFu) | ((uint32_t)(-8 * S[1].z) << 16);
                 uint32_t ctq = ct;
@@ -320,26 +327,41 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(4))) voi
                     const int x = lg + 8 * q;
                     const uint32_t mw = (x <= W[0] ? 0xFFFFu : 0u) | (x <= W[1] ? 0xFFFF0000u : 0u);
                     const uint32_t s = vt[0][q] | (vt[1][q] << 16);
-                    G.top[x] = vsel((q == 0 ? m0 : mT) & mw, pk_lshr4(pk_add(s, ctq)), GB2);
+                    G.top[x] = vsel((q == 0 ? m0 : mT) & mw, dec(s, ctq), GB2);
                     ctq = pk_add(ctq, dx);
                 }
             } else {
                 // the stored S values as they are; the boundaries computed: column 0 S(i, 0) =
-                // C0 i, row 0 S(0, j) = R0 j (stripe 0's top row)
+                // C0 i, row 0 S(0, j) = R0 j (stripe 0's top row).  Flexible-fill pairs store H,
+                // whose S can pass int16 on long pairs: the window holds S - Sb instead, Sb the
+                // bias part of S at its corner (16 g, c0) (-ma c0 + gap (c0 - 16 g)), i.e. H
+                // - gap (i - 16 g) down the left column and H + (gap - ma) x along the top row
+                auto pack = [](int a0, int a1) { return ((uint32_t)a0 & 0xFFFFu) | ((uint32_t)a1 << 16); };
+                int sb[2], al[2], at[2];
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    sb[h] = S[h].fx ? -ma * c0[h] + gap * (c0[h] - 16 * g[h]) : 0;
+                    al[h] = S[h].fx ? -gap * (2 * lg + 1) : 0;  // the lane's first row
+                    at[h] = S[h].fx ? (gap - ma) * lg : 0;       // column x = lg
+                }
+                const uint32_t SB = pack(sb[0], sb[1]), AL = pack(al[0], al[1]), AT = pack(at[0], at[1]);
+                const uint32_t AG = pack(S[0].fx ? -gap : 0, S[1].fx ? -gap : 0);
+                const uint32_t AX = pack(S[0].fx ? 8 * (gap - ma) : 0, S[1].fx ? 8 * (gap - ma) : 0);
                 const int ir0 = 16 * g[0] + 2 * lg + 1, ir1 = 16 * g[1] + 2 * lg + 1;
-                const uint32_t cb = ((uint32_t)(C0 * ir0) & 0xFFFFu) | ((uint32_t)(C0 * ir1) << 16);
+                const uint32_t cb = pk_sub(pack(C0 * ir0, C0 * ir1), SB);
                 const uint32_t mE = (live[0] && c0[0] > 0 ? 0xFFFFu : 0u) | (live[1] && c0[1] > 0 ? 0xFFFF0000u : 0u);
-                gl0 = vsel(mE, l0, cb);
-                gl1 = vsel(mE, l1, pk_add(cb, rep16(C0)));
-                const uint32_t rowb = ((uint32_t)(R0 * (c0[0] + lg)) & 0xFFFFu) | ((uint32_t)(R0 * (c0[1] + lg)) << 16);
-                const uint32_t colb = ((uint32_t)(C0 * 16 * g[0]) & 0xFFFFu) | ((uint32_t)(C0 * 16 * g[1]) << 16);
-                uint32_t rq = rowb;
+                gl0 = vsel(mE, pk_add(l0, AL), cb);
+                gl1 = vsel(mE, pk_add(l1, pk_add(AL, AG)), pk_add(cb, rep16(C0)));
+                const uint32_t rowb = pk_sub(pack(R0 * (c0[0] + lg), R0 * (c0[1] + lg)), SB);
+                const uint32_t colb = pk_sub(pack(C0 * 16 * g[0], C0 * 16 * g[1]), SB);
+                uint32_t rq = rowb, aq = AT;
 #pragma unroll
                 for (int q = 0; q < 5; ++q) {
-                    const uint32_t s = vt[0][q] | (vt[1][q] << 16);
+                    const uint32_t s = pk_add(vt[0][q] | (vt[1][q] << 16), aq);
                     const uint32_t alt = q == 0 ? vsel(mT, colb, rq) : rq;  // (q > 0: column > 0)
                     G.top[lg + 8 * q] = vsel(q == 0 ? m0 : mT, s, alt);
                     rq = pk_add(rq, rep16(8 * R0));
+                    aq = pk_add(aq, AX);
                 }
             }
         }

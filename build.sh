@@ -46,6 +46,8 @@ for m in 0 1 2; do
   for c in 0 1; do
     cc "$B/ta_flex_$m$c.o" "$CS/ta_flex.hip" "$HIPCC" "${FLAGS[@]}" -DTA_FLEX_MODE=$m -DTA_FLEX_CIGAR=$c -c "$CS/ta_flex.hip"
   done
+  # ... with checkpoints instead of codes (checkpoint plans)
+  cc "$B/ta_flex_ck_$m.o" "$CS/ta_flex.hip" "$HIPCC" "${FLAGS[@]}" -DTA_FLEX_MODE=$m -DTA_FLEX_CIGAR=1 -DTA_FLEX_CK=1 -c "$CS/ta_flex.hip"
 done
 cc "$B/ta_misc.o" "$CS/ta_kernels.hip" "$HIPCC" "${FLAGS[@]}" -DTA_TU_MISC -c "$CS/ta_kernels.hip"
 # affine-gap extension (fill + traceback kernels and its plan driver)
@@ -66,7 +68,7 @@ done
 cc "$B/tm_main.o" "$CS/tm_main.cpp" "$HIPCC" "${FLAGS[@]}" -x c++ -c "$CS/tm_main.cpp"
 fi
 for p in "${pids[@]}"; do wait "$p"; done
-"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_dual_blk.o" "$B"/ta_dual_ck_{0,1,2}.o "$B/ta_walk_ck.o" "$B"/ta_flex_{0,1,2}{0,1}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_server.o" "$B/ta_planner.o" "$B/shim.o" \
+"$HIPCC" -shared -fPIC --offload-arch=gfx950 "$B"/ta_fill_{0,1,2}{0,1}.o "$B"/ta_dual_{0,1,2}{0,1}.o "$B/ta_dual_blk.o" "$B"/ta_dual_ck_{0,1,2}.o "$B/ta_walk_ck.o" "$B"/ta_flex_{0,1,2}{0,1}.o "$B"/ta_flex_ck_{0,1,2}.o "$B/ta_misc.o" "$B/ta_affine.o" "$B/ta_api.o" "$B/ta_server.o" "$B/ta_planner.o" "$B/shim.o" \
   -L/opt/rocm/lib -lrocprofiler-sdk-roctx -Wl,-rpath,/opt/rocm/lib -o "$OUT"
 if [ "${TA_LIB_ONLY:-0}" = 1 ]; then echo "built $OUT"; exit 0; fi
 PKG="$ROOT/bioinfo1_amd"

@@ -180,6 +180,7 @@ int ta_align_batch_flags(ta_context* ctx, uint32_t n_pairs, const char* query_by
 #define TA_PLAN_NO_CK 256u        /* those plans: the fill writes blocked codes walked by the band walks, never
                                      checkpoints walked by the recomputing walks (the default for large batches) */
 #define TA_PLAN_CK 512u           /* those plans: checkpoints and recomputing walks at any batch size */
+#define TA_PLAN_NO_FLEX_CK 1024u  /* plans with couples of different shapes: codes and the code walks, not checkpoints */
 int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_host,
                    const uint32_t* target_len_host, int type, int match, int mismatch, int gap, int want_cigar,
                    uint64_t workspace_budget, uint32_t flags, ta_plan** out);

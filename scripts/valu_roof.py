@@ -45,6 +45,8 @@ KERNELS = {
                                          "dual_fill_kernelILi2ELb1ELb0E"),
     "flex_fill_kernel<2, true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=2", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi2ELb1E"),
     "flex_fill_kernel<1, true>": ("ta_flex.hip", ["-DTA_FLEX_MODE=1", "-DTA_FLEX_CIGAR=1"], "flex_fill_kernelILi1ELb1E"),
+    "flex_fill_ck_kernel<2>": ("ta_flex.hip", ["-DTA_FLEX_MODE=2", "-DTA_FLEX_CIGAR=1", "-DTA_FLEX_CK=1"], "flex_fill_ck_kernelILi2E"),
+    "flex_fill_ck_kernel<1>": ("ta_flex.hip", ["-DTA_FLEX_MODE=1", "-DTA_FLEX_CIGAR=1", "-DTA_FLEX_CK=1"], "flex_fill_ck_kernelILi1E"),
     "affine_dual_fill_kernel<2, true>": ("ta_affine.hip", [], "affine_dual_fill_kernelILi2ELb1E"),
 }
 

@@ -305,8 +305,12 @@ void check_small_batches() {
                     const bool all_packed = ta::fits_int16(type, sh[0], sh[1], 1, -1, -1) && (packed || P % 2 == 0);
                     // global / semi: checkpoints (blocked region sizes) whenever they are taken
                     const bool edge_ck = all_packed && type != ta::kLocal && flags == 512u;
+                    // pairs past int16 in the dual kernel: flexible couples (self-coupled when alone),
+                    // with checkpoints under TA_PLAN_CK when their H fits (ta_planner.cpp flex_ck_fits)
+                    const bool flex_ck = flags == 512u && !ta::fits_int16(type, sh[0], sh[1], 1, -1, -1) &&
+                                         ta::flex_ck_fits(type, sh[0], sh[1], 1, -1, -1);
                     CHECK(pl.blk == ((all_packed && type == ta::kLocal && P >= 8 && flags != 128u && sh[0] + sh[1] <= 6000) ||
-                                     edge_ck));
+                                     edge_ck || flex_ck));
                     // checkpoints and recomputing walks: small batches only with TA_PLAN_CK (gap -1 <= 0)
                     CHECK(pl.ck == (pl.blk && flags == 512u));
                     if (pl.ck) CHECK(pl.walk_group == 64);

@@ -647,6 +647,48 @@ def test_ck_walk_edge(aligner, oracle, mode, sc):
         assert got.cigar(p) == want.cigar(p), (mode, sc, p, b.qlen[p], b.tlen[p])
 
 
+@pytest.mark.parametrize("mode,sc", [(m, s) for m in (0, 1, 2) for s in ((1, -1, -1), (2, -3, -1), (3, 4, 0))])
+def test_ck_walk_flex(aligner, oracle, mode, sc):
+    """Checkpoints of the flexible fill (couples of different shapes, H itself in the
+    checkpoints) walked by the recomputing walk, against the oracle: every mode, ragged
+    couples of one to three passes, pairs coupled with themselves, long I and D runs,
+    queries with other letters than A, C, G, T (the fill's non-table path) and a '-' in a
+    target (the couple handed back to the int32 fill and the one-pair walk)."""
+    if mode == 1 and sc[2] > 0:
+        pytest.skip("local checkpoint walks need gap <= 0")
+    rng = np.random.default_rng(0xF1E + 13 * mode + 5 * sc[0] - sc[1])
+    al = np.frombuffer(b"ACGT", np.uint8)
+    rnd = lambda k: al[rng.integers(4, size=k)].tobytes()  # noqa: E731
+    pairs = []
+    # (n, m of each couple's pairs): same pass count and n mod 16 within a group, so the
+    # planner couples them; m within 25 % of waste
+    for n, ms in ((517, (600, 520, 480, 555, 610)), (1030, (990, 1100, 940)), (2100, (700, 640, 690)),
+                  (300, (260, 280, 300, 240))):
+        for k, m in enumerate(ms):
+            core = rnd(min(n, m) - 60)
+            gapb = b"N" * (30 + 17 * k)
+            if k % 3 == 0:  # an insertion in the target: an I run
+                q, t = core, core[: len(core) // 2] + gapb + core[len(core) // 2:]
+            elif k % 3 == 1:  # a deletion: a D run
+                q, t = core[: len(core) // 3] + gapb + core[len(core) // 3:], core
+            else:
+                q, t = rnd(n), rnd(m)
+            q, t = (q + rnd(max(0, n - len(q))))[:n], (t + rnd(max(0, m - len(t))))[:m]
+            pairs.append((q, t))
+    pairs.append((b"ACGTN" * 103 + b"AC", rnd(530)))  # a query letter past A, C, G, T (n = 517)
+    pairs.append((rnd(517), rnd(200) + b"-" + rnd(300)))  # a free gap step in a target
+    b = synth.from_pairs(pairs)
+    plan = DevicePlan(aligner, b, mode, *sc, True, flags=TA_PLAN_CK)
+    assert plan.ck and plan.walk == 64 and plan.flex_pairs > 0, (plan.blk, plan.ck, plan.walk, plan.flex_pairs)
+    plan.close()
+    want = oracle.align_batch(b, mode, *sc, True)
+    got = run_plan(aligner, b, mode, sc, True, TA_PLAN_CK)
+    np.testing.assert_array_equal(got.scores, want.scores)
+    np.testing.assert_array_equal(got.target_begins, want.target_begins)
+    for p in range(b.n_pairs):
+        assert got.cigar(p) == want.cigar(p), (mode, sc, p, b.qlen[p], b.tlen[p])
+
+
 def test_local_walk_long_runs(aligner, oracle):
     """Local paths with long gap and match runs (past the group walk's 32-cell
     clip and the one-pair walk's 64-cell windows) across pass and tile edges
