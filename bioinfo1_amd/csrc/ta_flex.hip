@@ -87,6 +87,9 @@ struct FlexIo {
     uint32_t tag_w, tag_r;
     uint32_t* err;
     uint32_t* cbuf;  // CK: this wave's LDS staging of 16 steps' bottom rows, [step][lane]
+    // this wave's per-step operands of the current 64 steps, entry k for step 64c + k: both
+    // pairs' mismatch tables of the new target byte, the row above, the bytes (flex_pass)
+    uint4* lst;
 };
 
 struct FlexOut {
@@ -178,17 +181,44 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     int rb[2] = {INT_MIN, INT_MIN};
     uint32_t rbj[2] = {0, 0};
 
-    uint32_t tcur[2], tnext[2];
+    // A step's wave-uniform operands -- both pairs' mismatch tables of the new target byte,
+    // the row above, the raw bytes -- come from one LDS read of a 64-entry list each lane
+    // fills for its column every 64 steps (after the rebase: the row above is stored
+    // relative to the chunk's O), instead of v_readlane and SALU table arithmetic per step
+    // (as ta_dual.hip LST); the DPP hand-offs take the read registers as their lane-0 value
+    uint32_t tnext[2];
+    auto tbyte = [&](int h, uint32_t c) -> uint32_t {  // target byte of step 64c + lane
+        const uint32_t k = c * 64u + (uint32_t)lane;
+        return k < io.m[h] ? (uint32_t)io.T[h][k] : 0u;
+    };
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        tcur[h] = load_tchunk(io.T[h], io.m[h], 0, lane);
-        tnext[h] = load_tchunk(io.T[h], io.m[h], 1, lane);
-    }
+    for (int h = 0; h < 2; ++h) tnext[h] = tbyte(h, 0);
     // the previous pass's bottom row, polled one 64-column chunk at a time just
     // before it is needed (no prefetch of the next chunk: that would make every
     // pass trail its predecessor by one more chunk)
     int bcur[2] = {0, 0};
     if (pass > 0) load_rec_chunk(io, M, 0, lane, bcur);
+    // the list of chunk c (its bytes in tnext; the row above: pass 0 S(0, j), later passes
+    // the polled records, less dl -- added back by the hand-off -- and O)
+    auto lst_fill = [&](uint32_t c) {
+        const int j = (int)(c * 64u) + lane + 1;
+        int ta, tb;
+        if (pass == 0) {
+            const int s0 = (init - ma + rowb) * j - dl;
+            ta = s0 - O[0];
+            tb = s0 - O[1];
+        } else {
+            ta = bcur[0] - dl - O[0];
+            tb = bcur[1] - dl - O[1];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (after the last chunk's reads)
+        io.lst[lane] = make_uint4(mismatch_table(tnext[0]), mismatch_table(tnext[1]),
+                                  ((uint32_t)ta & 0xFFFFu) | ((uint32_t)tb << 16), tnext[0] | (tnext[1] << 16));
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int h = 0; h < 2; ++h) tnext[h] = tbyte(h, c + 1);
+    };
+    lst_fill(0);
     const uint32_t steps = M + nl - 1;
     const uint32_t Tmax0 = pass_steps(io.m[0]), Tmax1 = pass_steps(io.m[1]);
     // CK: each pair's blocks of this pass (ta_layout.h ck_row_index: nb_h * 1024 dwords a pass)
@@ -245,13 +275,6 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     };
 
     auto reload = [&](uint32_t t) {
-        if ((t & 255u) == 0) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                tcur[h] = tnext[h];
-                tnext[h] = load_tchunk(io.T[h], io.m[h], (t >> 8) + 1, lane);
-            }
-        }
         if (pass > 0) {
             load_rec_chunk(io, M, t >> 6, lane, bcur);
         }
@@ -264,6 +287,7 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
         if (LOCAL) zu = C0;
         O[0] += sext_lo(d);
         O[1] += sext_hi(d);
+        lst_fill(t >> 6);
     };
     auto capture = [&](int h, int j, bool active) {
         // lanes at column m_h: this pass's column-m candidates (semi) or the corner (global)
@@ -289,27 +313,16 @@ __device__ __forceinline__ FlexOut flex_pass(const FillArgs& a, const FlexIo& io
     };
     auto step = [&](uint32_t t, auto masked_tag) {
         constexpr bool MASKED = decltype(masked_tag)::value;
-        uint32_t top;
-        if (pass == 0) {
-            const int s0 = (init - ma + rowb) * (int)(t + 1) - dl;  // S(0, j) (local: - dl, added back by the hand-off)
-            top = ((uint32_t)(s0 - O[0]) & 0xFFFFu) | ((uint32_t)(s0 - O[1]) << 16);
-        } else {
-            const int ba = rdlane(bcur[0], t & 63u) - dl, bb = rdlane(bcur[1], t & 63u) - dl;
-            top = ((uint32_t)(ba - O[0]) & 0xFFFFu) | ((uint32_t)(bb - O[1]) << 16);
-        }
-        const uint32_t sh = (t & 3u) * 8;
-        const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
-        const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
-        const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
+        const uint4 e = io.lst[t & 63u];  // (one address for the wave: a broadcast)
         const uint32_t prev = recv;
-        recv = (uint32_t)wave_shr1((int)top, (int)H2[R - 1]);
+        recv = (uint32_t)wave_shr1((int)e.z, (int)H2[R - 1]);
         if constexpr (LOCAL) recv = pk_add(recv, D2);  // into this lane's frame
         if constexpr (CLS) {
-            tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
-            tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
-            if (tdash) tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+            tA = (uint32_t)wave_shr1((int)e.x, (int)tA);
+            tB = (uint32_t)wave_shr1((int)e.y, (int)tB);
+            if (tdash) tc2 = (uint32_t)wave_shr1((int)e.w, (int)tc2);
         } else {
-            tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+            tc2 = (uint32_t)wave_shr1((int)e.w, (int)tc2);
         }
         if (LOCAL) zu += gap - ma;
 
@@ -513,6 +526,7 @@ __device__ __forceinline__ void flex_fill_body(FillArgs a) {
     const int lane = threadIdx.x & 63;
     constexpr bool CK = kFlexCk && CIGAR;
     __shared__ uint32_t cbuf_all[CK ? kWavesPerBlock * 16 * kWave : 1];
+    __shared__ uint4 lst_all[kWavesPerBlock * 64];  // (flex_pass: the per-step operands)
     uint32_t tk = 0;
     if (lane == 0) tk = atomicAdd(a.ticket, 1u);
     tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
@@ -575,6 +589,7 @@ __device__ __forceinline__ void flex_fill_body(FillArgs a) {
     io.tag_r = a.epoch * 64u + pass;
     io.err = a.err;
     io.cbuf = cbuf_all + (CK ? (threadIdx.x >> 6) * 16 * kWave : 0);
+    io.lst = lst_all + (threadIdx.x >> 6) * 64;
     const FlexOut o = __ballot(qother) == 0 ? flex_pass_nv<MODE, CIGAR, true>(a, io, pass, last_pass, tdash, lane)
                                             : flex_pass_nv<MODE, CIGAR, false>(a, io, pass, last_pass, tdash, lane);
     if (lane == 0) {
