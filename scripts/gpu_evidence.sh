@@ -7,7 +7,7 @@ set -u
 mkdir -p gpurun_out
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }
 declare -A RUN=(
-  [cfg2]="--steps 10 --warmup 2"
+  [cfg2]=""  # (bench.py defaults: the driver's own run)
   [cfg3]="--workload cfg3 --steps 3 --warmup 1"
   [cfg3_local]="--workload cfg3 --mode local --steps 3 --warmup 1"
   [cfg3map]="--workload cfg3map --steps 2 --warmup 1"
