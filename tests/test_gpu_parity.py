@@ -689,6 +689,29 @@ def test_ck_walk_flex(aligner, oracle, mode, sc):
         assert got.cigar(p) == want.cigar(p), (mode, sc, p, b.qlen[p], b.tlen[p])
 
 
+def test_ck_walk_long_free_run(aligner, oracle):
+    """gap = 0 (local walks over checkpoints allow it): a free insertion of 9,000 target
+    columns inside the local path, an I run that crosses ~560 windows and passes the
+    event's 14-bit count (8,192: the walk splits it), plus a long free
+    deletion in a second pair; against the oracle."""
+    rng = np.random.default_rng(0x8192)
+    al = np.frombuffer(b"ACGT", np.uint8)
+    core = al[rng.integers(4, size=240)].tobytes()
+    pairs = [(core, core[:120] + b"N" * 9000 + core[120:]),   # I run of 9,000
+             (core[:90] + b"N" * 8500 + core[90:], core)]     # D run of 8,500
+    b = synth.from_pairs(pairs)
+    sc = (2, -3, 0)
+    plan = DevicePlan(aligner, b, 1, *sc, True, flags=TA_PLAN_CK)
+    assert plan.ck and plan.walk == 64, (plan.blk, plan.ck, plan.walk)
+    plan.close()
+    want = oracle.align_batch(b, 1, *sc, True)
+    got = run_plan(aligner, b, 1, sc, True, TA_PLAN_CK)
+    np.testing.assert_array_equal(got.scores, want.scores)
+    np.testing.assert_array_equal(got.target_begins, want.target_begins)
+    for p in range(b.n_pairs):
+        assert got.cigar(p) == want.cigar(p), (p, got.cigar(p)[:60], want.cigar(p)[:60])
+
+
 def test_local_walk_long_runs(aligner, oracle):
     """Local paths with long gap and match runs (past the group walk's 32-cell
     clip and the one-pair walk's 64-cell windows) across pass and tile edges
