@@ -622,6 +622,10 @@ struct AffRec {
     const uint64_t* r;  // the previous pass's (null on pass 0)
     uint32_t tag_w, tag_r;
     uint32_t* err;
+    // this wave's per-step operands of the current 64 steps (aff_dual_pass): entry k for
+    // step 64c + k -- both pairs' mismatch tables, the row above (H, F) -- and the bytes
+    uint4* lst;
+    uint32_t* lstc;
 };
 
 // columns 64k + lane + 1 of the previous pass's bottom row: (H, F) packed
@@ -706,55 +710,56 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
     uint32_t jj = rep16(-lane);
     uint32_t rowbest = rep16(-32768), rowbest_j = 0;
 
-    uint32_t tcur[2], tnext[2];
+    // A step's wave-uniform operands come from one LDS read of a 64-entry list each lane
+    // fills for its column every 64 steps, instead of v_readlane and SALU tables per step
+    // (ta_dual.hip LST)
+    uint32_t tnext[2];
+    auto tbyte = [&](int h, uint32_t c) -> uint32_t {  // target byte of step 64c + lane
+        const uint32_t k = c * 64u + (uint32_t)lane;
+        return k < m ? (uint32_t)T[h][k] : 0u;
+    };
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-        tcur[h] = load_tchunk(T[h], m, 0, lane);
-        tnext[h] = load_tchunk(T[h], m, 1, lane);
-    }
+    for (int h = 0; h < 2; ++h) tnext[h] = tbyte(h, 0);
     // the previous pass's bottom row, polled one 64-column chunk at a time just
     // before it is needed
     uint2 bcur = make_uint2(0, 0);
     if (pass > 0) bcur = aff_poll_chunk(rc, m, 0, lane);
+    auto lst_fill = [&](uint32_t c) {
+        uint32_t tH = bcur.x, tF = bcur.y;
+        if (pass == 0) {  // row 0 (:89-92 with an affine gap): H(0,j) - ma*j; F(0,j) = -inf stand-in
+            const int jt = (int)(c * 64u) + lane + 1;
+            const int h0 = ((MODE == kGlobal) ? O + jt * X : 0) - ma * jt + X * jt;
+            tH = rep16(h0);
+            tF = rep16(h0 - K);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // (after the last chunk's reads)
+        rc.lst[lane] = make_uint4(mismatch_table(tnext[0]), mismatch_table(tnext[1]), tH, tF);
+        rc.lstc[lane] = tnext[0] | (tnext[1] << 16);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+#pragma unroll
+        for (int h = 0; h < 2; ++h) tnext[h] = tbyte(h, c + 1);
+    };
+    lst_fill(0);
     const uint32_t steps = m + nl - 1;
     uint2* prow0 = CIGAR ? ptrs[0] + (uint64_t)pass * Tmax * kWave : nullptr;
     uint2* prow1 = CIGAR ? ptrs[1] + (uint64_t)pass * Tmax * kWave : nullptr;
 
     auto reload = [&](uint32_t t) {
-        if ((t & 255u) == 0) {
-#pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                tcur[h] = tnext[h];
-                tnext[h] = load_tchunk(T[h], m, (t >> 8) + 1, lane);
-            }
-        }
         if (pass > 0) bcur = aff_poll_chunk(rc, m, t >> 6, lane);
+        lst_fill(t >> 6);
     };
     auto step = [&](uint32_t t, auto masked_tag) {
         constexpr bool MASKED = decltype(masked_tag)::value;
-        uint32_t topH, topF;
-        if (pass == 0) {  // row 0 (:89-92 with an affine gap): H(0,j) - ma*j; F(0,j) = -inf stand-in
-            const int jt = (int)t + 1;
-            const int h0 = ((MODE == kGlobal) ? O + jt * X : 0) - ma * jt + X * jt;
-            topH = rep16(h0);
-            topF = rep16(h0 - K);
-        } else {
-            topH = (uint32_t)rdlane((int)bcur.x, t & 63u);
-            topF = (uint32_t)rdlane((int)bcur.y, t & 63u);
-        }
-        const uint32_t sh = (t & 3u) * 8;
-        const uint32_t wa = (uint32_t)rdlane((int)tcur[0], (t >> 2) & 63u);
-        const uint32_t wb = (uint32_t)rdlane((int)tcur[1], (t >> 2) & 63u);
-        const uint32_t newc = ((wa >> sh) & 0xFFu) | (((wb >> sh) & 0xFFu) << 16);
+        const uint4 e = rc.lst[t & 63u];  // (one address for the wave: a broadcast)
         const uint32_t prev = recvH;
-        recvH = (uint32_t)wave_shr1((int)topH, (int)H2[R - 1]);
-        recvF = (uint32_t)wave_shr1((int)topF, (int)Flast);
+        recvH = (uint32_t)wave_shr1((int)e.z, (int)H2[R - 1]);
+        recvF = (uint32_t)wave_shr1((int)e.w, (int)Flast);
         if constexpr (CLS) {
-            tA = (uint32_t)wave_shr1((int)mismatch_table((wa >> sh) & 0xFFu), (int)tA);
-            tB = (uint32_t)wave_shr1((int)mismatch_table((wb >> sh) & 0xFFu), (int)tB);
-            if (tdash) tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+            tA = (uint32_t)wave_shr1((int)e.x, (int)tA);
+            tB = (uint32_t)wave_shr1((int)e.y, (int)tB);
+            if (tdash) tc2 = (uint32_t)wave_shr1((int)rc.lstc[t & 63u], (int)tc2);
         } else {
-            tc2 = (uint32_t)wave_shr1((int)newc, (int)tc2);
+            tc2 = (uint32_t)wave_shr1((int)rc.lstc[t & 63u], (int)tc2);
         }
         jj = pk_add(jj, ONE);
         if (MODE == kSemi) maj = pk_add(maj, MA2);
@@ -824,7 +829,7 @@ __device__ __forceinline__ void aff_dual_pass(const AffArgs& a, const uint8_t* c
         }
     };
     const uint32_t ramp_end = min(nl - 1, steps);
-    const uint32_t every = (pass > 0) ? 64u : 256u;
+    const uint32_t every = 64u;  // (the operand list's chunks)
     uint32_t t = 0, next_reload = every;
     auto run_steps = [&](uint32_t t_end, auto masked_tag) {
         while (t < t_end) {
@@ -907,6 +912,8 @@ constexpr uint32_t kAffSkip = 0xFFFFFFFFu;  // PassOut.i of a couple handed to t
 template <int MODE, bool CIGAR>
 __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) void affine_dual_fill_kernel(AffArgs a) {
     const int lane = threadIdx.x & 63;
+    __shared__ uint4 lst_all[kWavesPerBlock * 64];  // (aff_dual_pass: the per-step operands)
+    __shared__ uint32_t lstc_all[kWavesPerBlock * 64];
     uint32_t tk = 0;
     if (lane == 0) tk = atomicAdd(a.ticket, 1u);
     tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
@@ -965,6 +972,8 @@ __global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) voi
     rc.tag_w = a.epoch * 64u + pass + 1u;
     rc.tag_r = a.epoch * 64u + pass;
     rc.err = a.err;
+    rc.lst = lst_all + (threadIdx.x >> 6) * 64;
+    rc.lstc = lstc_all + (threadIdx.x >> 6) * 64;
     PassOut o[2];
     if (cls) aff_dual_pass_nv<MODE, CIGAR, true>(a, Q, T, ptrs, rc, n, m, pass, last_pass, tdash, lane, o);
     else aff_dual_pass_nv<MODE, CIGAR, false>(a, Q, T, ptrs, rc, n, m, pass, last_pass, tdash, lane, o);
