@@ -350,9 +350,12 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
     uint64_t len_sum = 0;
     for (uint32_t p = 0; p < n_pairs; ++p) len_sum += (uint64_t)qlen[p] + tlen[p];
     const bool short_pairs = len_sum <= 6000ull * std::max<uint32_t>(n_pairs, 1);
-    // (batches of fewer than 8 pairs -- drop-in calls -- keep the lane walks: one band-walk
-    // lane per pair leaves a lone wave's dependent chain ~50 us longer for 1-2 pairs of
-    // 1 kb, scripts/exp/batch_latency.py, profiles/bench/r05_batch_latency.txt)
+    // Local plans take the blocked layout only with checkpoints (ck_size, gap <= 0) or
+    // under TA_PLAN_NO_CK (blocked codes and band walks): below the checkpoint size the
+    // [step][lane] codes (whose fill reads its per-step operands from the LDS list) and
+    // the lane walks finish sooner at every batch size measured, 8-4096 pairs of
+    // 200-1000 bases (3-6 %, scripts/exp/batch_latency.py, profiles/bench/r06s_batch_latency.txt).
+    // (Batches of fewer than 8 pairs keep the lane walks with any flag.)
     bool all_dual = !units.empty(), all_packed = !units.empty(), any_flex = false;
     for (const Unit& u : units) {
         all_dual = all_dual && u.kind == 1;
@@ -374,7 +377,8 @@ void build_plan(Plan& pl, uint32_t n_pairs, const uint32_t* qlen, const uint32_t
                        flex_ck_fits(type, qlen[u.b], tlen[u.b], match, mismatch, gap);
     const bool flex_ck = ck_want && any_flex && all_packed && flex_fit && !(flags & kPlanNoFlexCk);
     pl.blk = (want_cigar && type == kLocal && all_dual && short_pairs && n_pairs >= 8 && mag < (1ull << 22) &&
-              !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2))) || edge_ck || flex_ck;
+              ((flags & kPlanNoCk) || (ck_size && gap <= 0)) && !(flags & (kPlanNoBlk | kPlanWalk1 | kPlanWalk2))) ||
+             edge_ck || flex_ck;
     // Multi-pass int32 pairs run one wave per (pair, pass) like the packed
     // fills (their passes overlap instead of following each other on one
     // wave); the walk then runs in the traceback kernel.

@@ -297,6 +297,7 @@ void check_small_batches() {
                                     pl.chunks.size());
                     // every pair in the packed kernels (an odd one coupled with itself) when it fits
                     // int16 and is not tiny (or TA_PLAN_CK); band walks (blocked layout) from 8 local pairs up
+                    // under TA_PLAN_NO_CK
                     const bool packed = ((uint64_t)sh[0] * sh[1] >= 4096 || flags == 512u) &&
                                         ta::fits_int16(type, sh[0], sh[1], 1, -1, -1);
                     // (n_dual_pairs counts two per couple, a self-coupled pair included)
@@ -309,7 +310,9 @@ void check_small_batches() {
                     // with checkpoints under TA_PLAN_CK when their H fits (ta_planner.cpp flex_ck_fits)
                     const bool flex_ck = flags == 512u && !ta::fits_int16(type, sh[0], sh[1], 1, -1, -1) &&
                                          ta::flex_ck_fits(type, sh[0], sh[1], 1, -1, -1);
-                    CHECK(pl.blk == ((all_packed && type == ta::kLocal && P >= 8 && flags != 128u && sh[0] + sh[1] <= 6000) ||
+                    // local: blocked codes only under TA_PLAN_NO_CK, or with checkpoints (TA_PLAN_CK)
+                    CHECK(pl.blk == ((all_packed && type == ta::kLocal && P >= 8 && (flags == 256u || flags == 512u) &&
+                                      sh[0] + sh[1] <= 6000) ||
                                      edge_ck || flex_ck));
                     // checkpoints and recomputing walks: small batches only with TA_PLAN_CK (gap -1 <= 0)
                     CHECK(pl.ck == (pl.blk && flags == 512u));

@@ -502,14 +502,18 @@ def test_band_walk(aligner, oracle, case):
         pairs += [(rb.query(p), rb.target(p)) for p in range(rb.n_pairs)]
     b = synth.from_pairs(pairs)
     plan = DevicePlan(aligner, b, 1, *sc, True)
-    assert plan.blk and plan.walk == walk and not plan.ck, (plan.blk, plan.walk, plan.ck)  # (small: band walks)
+    assert not plan.blk and plan.walk == 16, (plan.blk, plan.walk, plan.ck)  # (small: codes and lane walks)
+    plan.close()
+    # TA_PLAN_NO_CK: blocked codes and band walks
+    plan = DevicePlan(aligner, b, 1, *sc, True, flags=TA_PLAN_NO_CK)
+    assert plan.blk and plan.walk == walk and not plan.ck, (plan.blk, plan.walk, plan.ck)
     plan.close()
     # TA_PLAN_CK: checkpoints + recomputing walks (ta_walk_ck.hip) when walked with gap <= 0
     plan = DevicePlan(aligner, b, 1, *sc, True, flags=TA_PLAN_CK)
     assert plan.blk and plan.walk == walk and plan.ck == (walk == 64), (plan.blk, plan.walk, plan.ck)
     plan.close()
     want = oracle.align_batch(b, 1, *sc, True)
-    for flags in (0, TA_PLAN_CK, TA_PLAN_NO_BLK):
+    for flags in (0, TA_PLAN_NO_CK, TA_PLAN_CK, TA_PLAN_NO_BLK):
         got = run_plan(aligner, b, 1, sc, True, flags)
         np.testing.assert_array_equal(got.scores, want.scores)
         np.testing.assert_array_equal(got.target_begins, want.target_begins)
