@@ -497,7 +497,11 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* qlen, cons
 
 uint64_t ta_plan_cigar_slots_bytes(const ta_plan* pl) { return pl ? pl->h.slots_bytes : 0; }
 uint64_t ta_plan_workspace_bytes(const ta_plan* pl) {
-    return pl ? (pl->h.ws_ptr_dwords + pl->h.ws_bnd_words) * 4ull : 0;
+    if (!pl) return 0;
+    const ta::Plan& h = pl->h;
+    // codes / checkpoints, pass-boundary rows, and the walks' event words (exec_chunk ws_runs)
+    const uint64_t runs = (h.walk_group == 64 && h.want_cigar) ? 4 * (h.slots_bytes + 4) : 0;
+    return (h.ws_ptr_dwords + h.ws_bnd_words) * 4ull + runs;
 }
 uint32_t ta_plan_chunks(const ta_plan* pl) { return pl ? (uint32_t)pl->h.chunks.size() : 0; }
 uint32_t ta_plan_dual_pairs(const ta_plan* pl) { return pl ? pl->h.n_dual_pairs : 0; }

@@ -187,7 +187,8 @@ int ta_plan_create(ta_context* ctx, uint32_t n_pairs, const uint32_t* query_len_
 void ta_plan_destroy(ta_plan* plan);
 /* Total bytes of the device CIGAR slot arena the caller must provide. */
 uint64_t ta_plan_cigar_slots_bytes(const ta_plan* plan);
-/* Device workspace held by the plan, and the number of launch chunks. */
+/* Device workspace a plan's execution grows in its context (codes or checkpoints,
+ * pass-boundary rows and the walks' event words), and the number of launch chunks. */
 uint64_t ta_plan_workspace_bytes(const ta_plan* plan);
 uint32_t ta_plan_chunks(const ta_plan* plan);
 /* Pairs the plan runs in the packed two-pairs-per-wave int16 kernels (equal
