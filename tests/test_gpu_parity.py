@@ -509,8 +509,12 @@ def test_band_walk(aligner, oracle, case):
     assert plan.blk and plan.walk == walk and not plan.ck, (plan.blk, plan.walk, plan.ck)
     plan.close()
     # TA_PLAN_CK: checkpoints + recomputing walks (ta_walk_ck.hip) when walked with gap <= 0
+    # (gap > 0: no checkpoints, so the codes and lane walks)
     plan = DevicePlan(aligner, b, 1, *sc, True, flags=TA_PLAN_CK)
-    assert plan.blk and plan.walk == walk and plan.ck == (walk == 64), (plan.blk, plan.walk, plan.ck)
+    if walk == 64:
+        assert plan.blk and plan.walk == 64 and plan.ck, (plan.blk, plan.walk, plan.ck)
+    else:
+        assert not plan.blk and plan.walk == 16 and not plan.ck, (plan.blk, plan.walk, plan.ck)
     plan.close()
     want = oracle.align_batch(b, 1, *sc, True)
     for flags in (0, TA_PLAN_NO_CK, TA_PLAN_CK, TA_PLAN_NO_BLK):
