@@ -273,11 +273,35 @@ int Align(const char* query, unsigned int query_len, const char* target, unsigne
     if (t != TA_GLOBAL && t != TA_LOCAL && t != TA_SEMI_GLOBAL)
         throw std::invalid_argument("Unknown AlignmentType provided.");  // team_alignment.cpp:73
     const int device = call_device();
-    // A lone large pair (>= 256k cells, no other call on the server) finishes
-    // sooner as a one-pair batch (the packed kernel, both halves computing it)
-    // than on one int32 wave; concurrent calls are better off on the server.
-    static std::atomic<int> in_server{0};
-    const bool lone_large = (uint64_t)query_len * target_len >= (1u << 18) && in_server.load() == 0;
+    // A large pair (>= 256k cells, no other call on the server) finishes sooner
+    // as a one-pair batch (the packed kernel, both halves computing it) than on
+    // one int32 wave, and so does a single caller's pair from ~45k cells
+    // (~212 x 212) up: 224 x 224 178 vs 200 us, 256 x 256 196 vs 226
+    // (profiles/bench/r06u_server_vs_batch.txt).  Concurrent calls of that size
+    // are better off on the server (16 threads of 256 x 256: 70k vs 52k calls/s),
+    // and a batch pauses the server: "single caller" means no call has had
+    // company in the last 100 ms, not just none at this instant (which sent a
+    // share of 8 threads' calls to the batch path, 256 x 256 35k -> 16k calls/s).
+    static std::atomic<int> in_server{0}, in_align{0};
+    static std::atomic<int64_t> last_company{INT64_MIN / 2};
+    struct Active {
+        std::atomic<int>& c;
+        int k;
+        explicit Active(std::atomic<int>& x) : c(x), k(x.fetch_add(1) + 1) {}
+        ~Active() { c.fetch_sub(1); }
+    } active(in_align);
+    const uint64_t cells = (uint64_t)query_len * target_len;
+    const bool mid = cells >= 45000 && cells < (1u << 18);
+    bool single = false;
+    if (mid || active.k > 1) {  // (a lone small call reads no clock)
+        const int64_t now = std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                std::chrono::steady_clock::now().time_since_epoch()).count();
+        // (refreshed every 10 ms at most: concurrent callers do not bounce the line per call)
+        if ((active.k > 1 || in_align.load() > 1) && now - last_company.load(std::memory_order_relaxed) > 10000000)
+            last_company.store(now);
+        single = mid && now - last_company.load() > 100000000;
+    }
+    const bool lone_large = (cells >= (1u << 18) && in_server.load() == 0) || single;
     if (server_enabled() && !lone_large) {
         ta_server* srv = server_for(device, t);
         if (srv && ta_server_fits(srv, query_len, target_len, match, mismatch, gap)) {
